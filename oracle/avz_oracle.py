@@ -1,0 +1,349 @@
+"""CPU restatement of the reference's mask-driven MVDR chain — TEST INFRASTRUCTURE ONLY.
+
+Imported only by ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg. The shipped path (``avz``) never calls into this module.
+
+Every function cites the reference line it restates (paths relative to
+/root/reference). The STFT/iSTFT live in a third-party dependency of the
+reference (``scipy.signal``; unpinned ``"scipy"`` in pyproject.toml:25, 1.15.3 in
+this image), restated here from scipy/signal/_spectral_py.py:
+
+* stft  -> _spectral_helper (boundary='zeros' :2050-2058, padded :2060-2067,
+  window cast :2083-2084, scale :2086-2094, _fft_helper :2158-2204,
+  result.astype(outdtype) :2141).
+* istft -> :1688-1729.
+
+Two flavours of the pipeline are provided:
+
+* ``*_loop``   — loop-faithful: the per-frequency Python loops of
+  rt_av_zoom/core/oracle_debug.py:56-80 and masked_mvdr.py:92-124.
+  This is the timed CPU baseline (``kind: "port"``).
+* ``*_vec``    — vectorised numpy restatement (same math, broadcast over bins),
+  used by tests as the fast checker.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# ----------------------------------------------------------------------------
+# constants of the reference (rt_av_zoom/core/masked_mvdr.py:9-18,
+# rt_av_zoom/core/oracle_debug.py:23-24, Final_pipeline/src/config.py:14-29)
+# ----------------------------------------------------------------------------
+FS = 16000
+D_CORE = 0.01           # masked_mvdr.py:10 (imported by oracle_debug.py:11-19)
+C_SOUND = 343.0         # masked_mvdr.py:11
+ANGLE_TARGET = 90.0     # masked_mvdr.py:12, oracle_debug.py:23
+SIGMA_ORACLE = 1.0      # oracle_debug.py:24
+SIGMA_HEURISTIC = 1e-7  # masked_mvdr.py:16
+FMIN_MVDR = 100.0       # oracle_debug.py:67, masked_mvdr.py:109
+
+
+# ----------------------------------------------------------------------------
+# window / framing
+# ----------------------------------------------------------------------------
+def hann_periodic(n: int) -> np.ndarray:
+    """scipy.signal.get_window('hann', n) (fftbins=True => periodic), float64.
+
+    Restates scipy/signal/windows/_windows.py general_cosine with a=[0.5, 0.5]
+    on linspace(-pi, pi, n+1)[:-1] (the 'sym=False' extension/truncation).
+    """
+    fac = np.linspace(-np.pi, np.pi, n + 1)[:-1]
+    return 0.5 + 0.5 * np.cos(fac)
+
+
+def n_frames(length: int, n_fft: int, hop: int) -> int:
+    """Frame count of scipy's stft with boundary='zeros', padded=True.
+
+    Lp = L + 2*(N//2); nadd = (-(Lp-N) % H) % N (_spectral_py.py:2063);
+    T = (Lp + nadd - N)//H + 1.
+    """
+    lp = length + 2 * (n_fft // 2)
+    nadd = (-(lp - n_fft) % hop) % n_fft
+    return (lp + nadd - n_fft) // hop + 1
+
+
+def stft(x: np.ndarray, fs: float = FS, nperseg: int = 512, noverlap: int = 256):
+    """Restatement of ``scipy.signal.stft(x, fs, nperseg=N, noverlap=O)`` as the
+    reference calls it (oracle_debug.py:42-44, masked_mvdr.py:76,
+    Final_pipeline/src/inference.py:198).
+
+    Returns (f, t, Y) with Y [..., F, T] in complex64 (result.astype(outdtype)).
+    """
+    x = np.asarray(x)
+    outdtype = np.result_type(x, np.complex64)
+    n = nperseg
+    hop = n - noverlap
+    win = hann_periodic(n)
+    win_c = win.astype(outdtype)                     # :2083-2084
+    scale = np.sqrt(1.0 / win_c.sum() ** 2)          # :2092 ('spectrum'), :2094 sqrt for stft
+    half = n // 2
+    zeros = np.zeros(x.shape[:-1] + (half,), dtype=x.dtype)
+    xe = np.concatenate((zeros, x, zeros), axis=-1)  # zero_ext
+    nadd = (-(xe.shape[-1] - n) % hop) % n           # :2063
+    xe = np.concatenate((xe, np.zeros(xe.shape[:-1] + (nadd,))), axis=-1)  # float64 promote
+    frames = np.lib.stride_tricks.sliding_window_view(xe, n, axis=-1)[..., ::hop, :]
+    res = win_c * frames                             # complex (fp64 x fp32-rounded window)
+    res = np.fft.rfft(res.real, n=n)                 # _fft_helper onesided
+    res = res * scale
+    res = res.astype(outdtype)
+    res = np.moveaxis(res, -1, -2)                   # [..., F, T]
+    f = np.fft.rfftfreq(n, 1.0 / fs)
+    t = np.arange(res.shape[-1]) * hop / float(fs)
+    return f, t, res
+
+
+def istft(S: np.ndarray, fs: float = FS, nperseg: int = 512, noverlap: int = 256):
+    """Restatement of ``scipy.signal.istft(S, fs, nperseg=N, noverlap=O)``
+    (_spectral_py.py:1688-1729): irfft, x win.sum(), windowed overlap-add,
+    N/2 trim, divide by the OLA of win**2 where > 1e-10. Returns (t, x)."""
+    S = np.asarray(S)
+    n = nperseg
+    hop = n - noverlap
+    nseg = S.shape[-1]
+    xsubs = np.fft.irfft(S, axis=-2, n=n)[..., :n, :]
+    win = hann_periodic(n)
+    if np.result_type(win, xsubs) != xsubs.dtype:
+        win = win.astype(xsubs.dtype)
+    xsubs = xsubs * win.sum()
+    outlen = n + (nseg - 1) * hop
+    x = np.zeros(S.shape[:-2] + (outlen,), dtype=xsubs.dtype)
+    norm = np.zeros(outlen, dtype=xsubs.dtype)
+    for ii in range(nseg):                           # :1708-1711 (per-frame OLA loop)
+        x[..., ii * hop: ii * hop + n] += xsubs[..., ii] * win
+        norm[ii * hop: ii * hop + n] += win ** 2
+    x = x[..., n // 2: -(n // 2)]
+    norm = norm[n // 2: -(n // 2)]
+    x /= np.where(norm > 1e-10, norm, 1.0)
+    return np.arange(x.shape[-1]) / float(fs), x.real
+
+
+# ----------------------------------------------------------------------------
+# masks, steering, covariance, solve
+# ----------------------------------------------------------------------------
+def steering_vector(angle_deg: float, f: float, d: float, c: float) -> np.ndarray:
+    """rt_av_zoom/core/masked_mvdr.py:22-35 — (2,1) complex128."""
+    theta = np.deg2rad(angle_deg)
+    phi = 0.0
+    tau1 = (d / 2) * np.cos(phi) * np.cos(theta - 0) / c
+    tau2 = (d / 2) * np.cos(phi) * np.cos(theta - np.pi) / c
+    omega = 2 * np.pi * f
+    return np.array([[np.exp(-1j * omega * tau1)], [np.exp(-1j * omega * tau2)]], dtype=complex)
+
+
+def steering_vectors(f_bins: np.ndarray, angle_deg: float, d: float, c: float) -> np.ndarray:
+    """Vectorised form (tf_lite_version/inference.py:53-81): [F, 2] complex128."""
+    theta = np.deg2rad(angle_deg)
+    tau1 = (d / 2) * np.cos(theta) / c
+    tau2 = (d / 2) * np.cos(theta - np.pi) / c
+    omega = 2 * np.pi * np.asarray(f_bins, dtype=np.float64)
+    return np.stack([np.exp(-1j * omega * tau1), np.exp(-1j * omega * tau2)], axis=-1)
+
+
+def ibm_mask_noise(S_tgt: np.ndarray, S_int: np.ndarray) -> np.ndarray:
+    """Oracle IBM, oracle_debug.py:49-53: 1.0 where |S_int| > |S_tgt| (strict)."""
+    return np.where(np.abs(S_int) > np.abs(S_tgt), 1.0, 0.0)
+
+
+def ipd_mask_noise(Y: np.ndarray) -> np.ndarray:
+    """Heuristic phase mask, masked_mvdr.py:37-46: 1.0 where |angle(Y0)-angle(Y1)| > 0
+    else 0.01 (angles of complex64 -> float32, difference in float32)."""
+    pd = np.angle(Y[0]) - np.angle(Y[1])
+    return np.where(np.abs(pd) > 0.0, 1.0, 0.01)
+
+
+def covariance_loop(Y: np.ndarray, mask_noise: np.ndarray) -> np.ndarray:
+    """Masked spatial covariance, oracle_debug.py:56-64 / masked_mvdr.py:92-102."""
+    n_ch, n_f, _ = Y.shape
+    R = np.zeros((n_f, n_ch, n_ch), dtype=complex)
+    for fi in range(n_f):
+        m_f = mask_noise[fi, :]
+        Y_f = Y[:, fi, :]
+        Yw = Y_f * np.sqrt(m_f)
+        R[fi] = (Yw @ Yw.conj().T) / (np.sum(m_f) + 1e-6)
+    return R
+
+
+def covariance_vec(Y: np.ndarray, mask_noise: np.ndarray, weight_eps: float = 0.0) -> np.ndarray:
+    """Same as covariance_loop, broadcast over bins (tf_lite_version/inference.py:103-127;
+    weight_eps=1e-10 reproduces that variant's sqrt(mask + 1e-10))."""
+    Yp = np.transpose(Y, (1, 0, 2))                    # F, M, T
+    w = np.sqrt(mask_noise + weight_eps)[:, None, :]
+    Yw = Yp * w
+    R = np.einsum('fmt,fnt->fmn', Yw, Yw.conj())
+    return R / (np.sum(mask_noise, axis=1)[:, None, None] + 1e-6)
+
+
+def mvdr_weights_loop(R: np.ndarray, f: np.ndarray, sigma: float, angle: float, d: float,
+                      c: float, fmin: float = FMIN_MVDR) -> np.ndarray:
+    """Per-bin MVDR solve, oracle_debug.py:66-79: w = solve(R+sigma I, d);
+    w /= (d^H w + 1e-10); LinAlgError -> [1, 0]; bins with f < fmin stay zero."""
+    n_f = R.shape[0]
+    W = np.zeros((n_f, 2), dtype=complex)
+    for fi in range(n_f):
+        if f[fi] < fmin:
+            continue
+        Rl = R[fi] + sigma * np.eye(2)
+        dv = steering_vector(angle, f[fi], d, c)
+        try:
+            w = np.linalg.solve(Rl, dv)
+            w /= (dv.conj().T @ w + 1e-10)
+        except np.linalg.LinAlgError:
+            w = np.array([[1], [0]])
+        W[fi] = w[:, 0]
+    return W
+
+
+def mvdr_weights_vec(R: np.ndarray, f: np.ndarray, sigma: float, angle: float, d: float,
+                     c: float, fmin: float = FMIN_MVDR) -> np.ndarray:
+    """Closed-form 2x2 Hermitian solve, broadcast over bins (same result as the loop)."""
+    dv = steering_vectors(f, angle, d, c)              # F, 2
+    a = R[:, 0, 0] + sigma
+    b = R[:, 0, 1]
+    cc = R[:, 1, 0]
+    e = R[:, 1, 1] + sigma
+    det = a * e - b * cc
+    ok = det != 0
+    safe = np.where(ok, det, 1.0)
+    w0 = (e * dv[:, 0] - b * dv[:, 1]) / safe
+    w1 = (a * dv[:, 1] - cc * dv[:, 0]) / safe
+    den = np.conj(dv[:, 0]) * w0 + np.conj(dv[:, 1]) * w1 + 1e-10
+    W = np.stack([w0 / den, w1 / den], axis=-1)
+    W[~ok] = np.array([1.0, 0.0])
+    W[np.asarray(f) < fmin] = 0.0
+    return W
+
+
+def apply_weights(W: np.ndarray, Y: np.ndarray) -> np.ndarray:
+    """S[f,t] = w^H Y[:, f, t] (oracle_debug.py:80)."""
+    return np.conj(W[:, 0])[:, None] * Y[0] + np.conj(W[:, 1])[:, None] * Y[1]
+
+
+# ----------------------------------------------------------------------------
+# end-to-end pipelines
+# ----------------------------------------------------------------------------
+def oracle_debug_loop(y_mix: np.ndarray, s_tgt: np.ndarray, s_int: np.ndarray, n_fft: int = 512,
+                      hop: int = 256, sigma: float = SIGMA_ORACLE, d: float = D_CORE,
+                      angle: float = ANGLE_TARGET, c: float = C_SOUND, fs: int = FS,
+                      normalize: bool = True) -> np.ndarray:
+    """rt_av_zoom/core/oracle_debug.py:27-97 minus file I/O (loop-faithful).
+
+    Note oracle_debug passes noverlap=N_HOP; with N_HOP = N/2 that is a hop of N/2."""
+    noverlap = n_fft - hop
+    f, _, Y = stft(y_mix, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    _, _, S_t = stft(s_tgt, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    _, _, S_i = stft(s_int, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    mask = ibm_mask_noise(S_t, S_i)
+    R = covariance_loop(Y, mask)
+    n_f, n_t = Y.shape[1], Y.shape[2]
+    S = np.zeros((n_f, n_t), dtype=complex)
+    for fi in range(n_f):                               # oracle_debug.py:66-80
+        if f[fi] < FMIN_MVDR:
+            continue
+        Rl = R[fi] + sigma * np.eye(2)
+        dv = steering_vector(angle, f[fi], d, c)
+        try:
+            w = np.linalg.solve(Rl, dv)
+            w /= (dv.conj().T @ w + 1e-10)
+        except Exception:  # bare except in the reference (:78)
+            w = np.array([[1], [0]])
+        S[fi, :] = w.conj().T @ Y[:, fi, :]
+    S_final = S * (1.0 - mask)                          # :84-90
+    _, s_out = istft(S_final, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    if normalize:
+        s_out = s_out / np.max(np.abs(s_out))           # :94
+    return s_out
+
+
+def oracle_debug_vec(y_mix, s_tgt, s_int, n_fft=512, hop=256, sigma=SIGMA_ORACLE, d=D_CORE,
+                     angle=ANGLE_TARGET, c=C_SOUND, fs=FS, normalize=True, return_stages=False):
+    """Vectorised restatement of oracle_debug.main (same math as the loop flavour)."""
+    noverlap = n_fft - hop
+    f, _, Y = stft(y_mix, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    _, _, S_t = stft(s_tgt, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    _, _, S_i = stft(s_int, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    mask = ibm_mask_noise(S_t, S_i)
+    R = covariance_vec(Y, mask)
+    W = mvdr_weights_vec(R, f, sigma, angle, d, c)
+    S_final = apply_weights(W, Y) * (1.0 - mask)
+    _, s_raw = istft(S_final, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    peak = np.max(np.abs(s_raw))
+    s_out = s_raw / peak if normalize else s_raw
+    if return_stages:
+        return s_out, dict(Y=Y, S_t=S_t, S_i=S_i, mask=mask, R=R, W=W, S_final=S_final,
+                           s_raw=s_raw, peak=peak, f=f)
+    return s_out
+
+
+def masked_mvdr_vec(y_mix, n_fft=512, hop=256, sigma=SIGMA_HEURISTIC, d=D_CORE,
+                    angle=ANGLE_TARGET, c=C_SOUND, fs=FS, normalize=True, return_stages=False):
+    """Heuristic IPD path, rt_av_zoom/core/masked_mvdr.py:50-132 minus I/O/plot:
+    IPD noise mask, covariance, MVDR (sigma=1e-7), no post-filter,
+    s /= (max|s| + 1e-6)."""
+    noverlap = n_fft - hop
+    f, _, Y = stft(y_mix, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    mask = ipd_mask_noise(Y)
+    R = covariance_vec(Y, mask)
+    W = mvdr_weights_vec(R, f, sigma, angle, d, c)
+    S = apply_weights(W, Y)
+    _, s_raw = istft(S, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    peak = np.max(np.abs(s_raw))
+    s_out = s_raw / (peak + 1e-6) if normalize else s_raw
+    if return_stages:
+        return s_out, dict(Y=Y, mask=mask, R=R, W=W, S=S, s_raw=s_raw, peak=peak, f=f)
+    return s_out
+
+
+def external_mask_vec(y_mix, mask_target, n_fft=1024, hop=512, sigma=1e-5, d=0.04,
+                      angle=ANGLE_TARGET, c=C_SOUND, fs=FS, floor=0.05, weight_eps=0.0,
+                      normalize=False):
+    """External (neural) target mask path, full_audio_generating_pipeline/inference.py:88-118
+    (process_chunk): noise mask 1-M, covariance, MVDR sigma=1e-5, post-filter max(M, 0.05).
+    ``floor=None`` disables the post-filter."""
+    noverlap = n_fft - hop
+    f, _, Y = stft(y_mix, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    mask_n = 1.0 - mask_target
+    R = covariance_vec(Y, mask_n, weight_eps)
+    W = mvdr_weights_vec(R, f, sigma, angle, d, c)
+    S = apply_weights(W, Y)
+    if floor is not None:
+        S = S * np.maximum(mask_target, floor)
+    _, s_raw = istft(S, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    if normalize:
+        return s_raw / np.max(np.abs(s_raw))
+    return s_raw
+
+
+# ----------------------------------------------------------------------------
+# metrics
+# ----------------------------------------------------------------------------
+def projection_sdr_sir(output, target, interf):
+    """scripts/run_metrics.py:6-36 (calculate_metrics_manual) -> (sdr, sir) in dB."""
+    eps = 1e-10
+    o = output / (np.linalg.norm(output) + eps)
+    t = target / (np.linalg.norm(target) + eps)
+    i = interf / (np.linalg.norm(interf) + eps)
+    alpha = np.dot(o, t)
+    beta = np.dot(o, i)
+    e_t = alpha * t
+    e_i = beta * i
+    e_a = o - e_t - e_i
+    p_t = np.sum(e_t ** 2)
+    p_i = np.sum(e_i ** 2) + 1e-10
+    p_n = np.sum(e_a ** 2) + 1e-10
+    return 10 * np.log10(p_t / (p_i + p_n)), 10 * np.log10(p_t / p_i)
+
+
+def osinr_osir(output, target, interf):
+    """Final_pipeline/src/metrics.py:102-123 (calculate_osnr_osir) -> (OSINR, OSIR)."""
+    eps = 1e-10
+    t = target / (np.linalg.norm(target) + eps)
+    i = interf / (np.linalg.norm(interf) + eps)
+    alpha = np.dot(output, t)
+    beta = np.dot(output, i)
+    e_t = alpha * t
+    e_i = beta * i
+    e_n = output - e_t - e_i
+    p_t = np.sum(e_t ** 2)
+    p_i = np.sum(e_i ** 2)
+    p_n = np.sum(e_n ** 2)
+    return 10 * np.log10(p_t / (p_i + p_n + eps)), 10 * np.log10(p_t / (p_i + eps))

@@ -1,0 +1,265 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
+
+Runs only in the build container (needs /root/reference, read-only). Nothing under
+tests/, bench.py or smoke() reads /root/reference at run time: they read the .npz
+files this script writes.
+
+How the reference is run:
+* ``soundfile`` (libsndfile) is not installed. A stand-in module is injected whose
+  ``read`` decodes the bundled int16 WAVs with scipy.io.wavfile and divides by 32768
+  (libsndfile's int16 -> float mapping), and whose ``write`` captures the float array
+  instead of quantising to PCM_16. It touches only file I/O, never the arithmetic.
+* matplotlib is forced to the Agg backend (masked_mvdr.main saves a PNG).
+* oracle_debug.main() reads a hard-coded OUTDIR (oracle_debug.py:25); we chdir to a
+  temp dir holding that folder. N_FFT/N_HOP/SIGMA are module globals we patch.
+* Intermediates are captured by wrapping scipy.signal.stft/istft and
+  numpy.linalg.solve for the duration of one reference call.
+
+Usage:  python tests/golden/make_golden.py      (writes tests/golden/*.npz)
+"""
+from __future__ import annotations
+
+import contextlib
+import json
+import os
+import shutil
+import sys
+import tempfile
+import types
+
+import numpy as np
+import scipy.io.wavfile as wavfile
+import scipy.signal
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+INPUTS = os.path.join(REF, "data", "inputs")
+
+TRIPLES = {
+    "test": ("test_mixture", "test_target_ref", "test_interferer_ref"),
+    "set2": ("mixture_3_sources_2", "target_reference_2", "interference_reference_2"),
+}
+STAGE_BINS = [4, 7, 64, 256]          # + F-1 appended per N
+
+
+# ----------------------------------------------------------------------------- stand-ins
+_WRITES: dict = {}
+
+
+def _sf_read(path, dtype="float64", **_kw):
+    fs, d = wavfile.read(path)
+    if d.dtype != np.int16:
+        raise ValueError(f"only int16 WAVs are expected, got {d.dtype} in {path}")
+    return (d.astype(np.float64) / 32768.0).astype(dtype), fs
+
+
+def _sf_write(path, data, fs, *_a, **_kw):
+    _WRITES[os.path.basename(str(path))] = np.array(data, copy=True)
+
+
+def install_reference():
+    sf = types.ModuleType("soundfile")
+    sf.read = _sf_read
+    sf.write = _sf_write
+    sys.modules["soundfile"] = sf
+    import matplotlib
+    matplotlib.use("Agg")
+    for p in (REF, os.path.join(REF, "scripts"), os.path.join(REF, "Final_pipeline")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from rt_av_zoom.core import masked_mvdr, oracle_debug  # noqa: F401
+    import run_metrics  # noqa: F401
+    from src import metrics  # noqa: F401  (Final_pipeline/src/metrics.py)
+    return oracle_debug, masked_mvdr, run_metrics, metrics
+
+
+@contextlib.contextmanager
+def capture():
+    """Wrap scipy.signal.stft/istft and np.linalg.solve; record their I/O."""
+    rec = {"stft": [], "istft": [], "solve": []}
+    o_stft, o_istft, o_solve = scipy.signal.stft, scipy.signal.istft, np.linalg.solve
+
+    def stft(*a, **k):
+        r = o_stft(*a, **k)
+        rec["stft"].append(r[2])
+        return r
+
+    def istft(*a, **k):
+        rec["istft_in"] = np.array(a[0], copy=True)
+        r = o_istft(*a, **k)
+        rec["istft"].append(np.array(r[1], copy=True))  # oracle_debug normalises in place
+        return r
+
+    def solve(A, b):
+        x = o_solve(A, b)
+        rec["solve"].append((np.array(A), np.array(b), np.array(x)))
+        return x
+
+    scipy.signal.stft, scipy.signal.istft, np.linalg.solve = stft, istft, solve
+    try:
+        yield rec
+    finally:
+        scipy.signal.stft, scipy.signal.istft, np.linalg.solve = o_stft, o_istft, o_solve
+
+
+def load_triple(name):
+    mix, tgt, itf = TRIPLES[name]
+    _, m = wavfile.read(os.path.join(INPUTS, mix + ".wav"))
+    _, t = wavfile.read(os.path.join(INPUTS, tgt + ".wav"))
+    _, i = wavfile.read(os.path.join(INPUTS, itf + ".wav"))
+    return m, t, i
+
+
+def run_oracle_debug(od, mix16, tgt16, int16_, n_fft, hop, sigma):
+    """Run the reference oracle_debug.main() on int16 arrays; return (out, rec)."""
+    with tempfile.TemporaryDirectory() as td:
+        outdir = os.path.join(td, od.OUTDIR)
+        os.makedirs(outdir)
+        wavfile.write(os.path.join(outdir, "mixture.wav"), 16000, mix16)
+        wavfile.write(os.path.join(outdir, "target_reference.wav"), 16000, tgt16)
+        wavfile.write(os.path.join(outdir, "interference_reference.wav"), 16000, int16_)
+        od.N_FFT, od.N_HOP, od.SIGMA = n_fft, hop, sigma
+        cwd = os.getcwd()
+        os.chdir(td)
+        _WRITES.clear()
+        try:
+            with contextlib.redirect_stdout(open(os.devnull, "w")), capture() as rec:
+                od.main()
+        finally:
+            os.chdir(cwd)
+        return _WRITES["output_oracle.wav"], rec
+
+
+def run_masked_mvdr(mm, mix16, n_fft, hop, sigma):
+    """Run the reference heuristic masked_mvdr.main(dir); return (out, rec)."""
+    with tempfile.TemporaryDirectory() as td:
+        world = os.path.join(td, "run", "World_Outputs")
+        os.makedirs(world)
+        wavfile.write(os.path.join(world, "mixture_3_sources.wav"), 16000, mix16)
+        mm.N_FFT, mm.N_HOP, mm.SIGMA = n_fft, hop, sigma
+        _WRITES.clear()
+        with contextlib.redirect_stdout(open(os.devnull, "w")), capture() as rec:
+            mm.main(world)
+        import matplotlib.pyplot as plt
+        plt.close("all")
+        return _WRITES["output_masked_mvdr.wav"], rec
+
+
+def stage_dict(rec, n_fft):
+    F = n_fft // 2 + 1
+    bins = STAGE_BINS + [F - 1]
+    Y = rec["stft"][0]
+    out = {"bins": np.array(bins), "Y_mix": Y[:, bins, :]}
+    if len(rec["stft"]) >= 3:
+        out["S_tgt"] = rec["stft"][1][bins, :]
+        out["S_int"] = rec["stft"][2][bins, :]
+    # solve() calls happen for bins with f >= 100 Hz, in order.
+    f = np.fft.rfftfreq(n_fft, 1 / 16000)
+    solved = [k for k in range(F) if f[k] >= 100]
+    A = np.stack([s[0] for s in rec["solve"]])
+    x = np.stack([s[2][:, 0] for s in rec["solve"]])
+    d = np.stack([s[1][:, 0] for s in rec["solve"]])
+    sel = [solved.index(k) for k in bins if k in solved]
+    out["solve_bins"] = np.array([k for k in bins if k in solved])
+    out["R_loaded"] = A[sel]
+    out["d"] = d[sel]
+    out["w_unnorm"] = x[sel]
+    out["S_final"] = rec["istft_in"][bins, :]
+    return out
+
+
+def main():
+    od, mm, run_metrics, metrics = install_reference()
+    manifest = {"generator": "tests/golden/make_golden.py", "reference": REF,
+                "scipy": scipy.__version__, "numpy": np.__version__, "files": {}}
+
+    def save(name, **arrays):
+        path = os.path.join(HERE, name)
+        np.savez_compressed(path, **arrays)
+        manifest["files"][name] = sorted(arrays)
+        print("wrote", name, os.path.getsize(path) // 1024, "KiB")
+
+    # -- bundled inputs (data files of the reference, int16) --------------------
+    trip = {k: load_triple(k) for k in TRIPLES}
+    for k, (m, t, i) in trip.items():
+        save(f"inputs_{k}.npz", mix=m, tgt=t, int=i)
+
+    # -- full-length oracle_debug runs ------------------------------------------
+    full_cases = [(k, n, s) for k in TRIPLES for n in (512, 1024) for s in (1.0, 1e-5, 1e-7)]
+    for k, n, s in full_cases:
+        m, t, i = trip[k]
+        out, rec = run_oracle_debug(od, m, t, i, n, n // 2, s)
+        raw = rec["istft"][0]
+        tf = t.astype(np.float32) / 32768.0
+        itf = i.astype(np.float32) / 32768.0
+        L = min(len(out), len(tf))
+        sdr_o, sir_o = run_metrics.calculate_metrics_manual(out[:L], tf[:L], itf[:L])
+        mix0 = m[:, 0].astype(np.float32) / 32768.0
+        sdr_i, sir_i = run_metrics.calculate_metrics_manual(mix0[:L], tf[:L], itf[:L])
+        osinr, osir = metrics.calculate_osnr_osir(out[:L].astype(np.float64),
+                                                  tf[:L].astype(np.float64),
+                                                  itf[:L].astype(np.float64))
+        save(f"full_{k}_n{n}_s{s:g}.npz", n_fft=n, hop=n // 2, sigma=s,
+             out_len=len(out), out_stride16=out[::16].astype(np.float32),
+             out_head=out[:4096].astype(np.float32), sumsq=np.sum(out ** 2),
+             peak_raw=np.max(np.abs(raw)), sir_in=sir_i, sdr_in=sdr_i, sir_out=sir_o,
+             sdr_out=sdr_o, osinr_out=osinr, osir_out=osir)
+
+    # -- 1.5-s excerpts (inputs = inputs_<k>.npz[seg]): full outputs + stage intermediates ----------------------
+    seg = slice(40000, 64000)
+    for k in TRIPLES:
+        m, t, i = trip[k]
+        m, t, i = m[seg], t[seg], i[seg]
+        for n in (512, 1024):
+            for s in (1.0, 1e-7):
+                out, rec = run_oracle_debug(od, m, t, i, n, n // 2, s)
+                arrays = dict(seg=np.array([seg.start, seg.stop]), n_fft=n, hop=n // 2, sigma=s,
+                              out=out.astype(np.float32), peak_raw=np.max(np.abs(rec["istft"][0])))
+                if k == "test":
+                    for key, v in stage_dict(rec, n).items():
+                        arrays["stage_" + key] = v
+                save(f"excerpt_{k}_n{n}_s{s:g}.npz", **arrays)
+
+    # -- heuristic IPD path (masked_mvdr.main) -----------------------------------
+    for k in TRIPLES:
+        m, t, i = trip[k]
+        for n in (512, 1024):
+            out, rec = run_masked_mvdr(mm, m, n, n // 2, 1e-7)
+            tf = t.astype(np.float32) / 32768.0
+            itf = i.astype(np.float32) / 32768.0
+            L = min(len(out), len(tf))
+            _, sir_o = run_metrics.calculate_metrics_manual(out[:L], tf[:L], itf[:L])
+            Y = rec["stft"][0]
+            ipd_mask = mm.compute_hard_geometric_mask(Y, None)
+            save(f"ipd_{k}_n{n}.npz", n_fft=n, hop=n // 2, sigma=1e-7, out_len=len(out),
+                 out_stride16=out[::16].astype(np.float32), out_head=out[:4096].astype(np.float32),
+                 sumsq=np.sum(out ** 2), sir_out=sir_o,
+                 mask_low_count=np.sum(ipd_mask < 1.0), mask_low_bins=np.nonzero(
+                     (ipd_mask < 1.0).any(axis=1))[0])
+        # excerpt with full output
+        mseg = m[seg]
+        for n in (512, 1024):
+            out, _ = run_masked_mvdr(mm, mseg, n, n // 2, 1e-7)
+            save(f"ipd_excerpt_{k}_n{n}.npz", seg=np.array([seg.start, seg.stop]), n_fft=n,
+                 hop=n // 2, sigma=1e-7, out=out.astype(np.float32))
+
+    # -- metric functions on fixed vectors ---------------------------------------
+    rng = np.random.default_rng(7)
+    o, t, i = rng.standard_normal((3, 5000))
+    o = 0.7 * t + 0.2 * i + 0.1 * o
+    sdr, sir = run_metrics.calculate_metrics_manual(o, t, i)
+    osinr, osir = metrics.calculate_osnr_osir(o, t, i)
+    save("metrics_vectors.npz", o=o, t=t, i=i, sdr=sdr, sir=sir, osinr=osinr, osir=osir)
+
+    # -- steering vectors --------------------------------------------------------
+    f = np.fft.rfftfreq(1024, 1 / 16000)
+    sv = np.stack([mm.get_steering_vector(a, fk, d, 343.0)[:, 0]
+                   for a, d in ((90.0, 0.01), (40.0, 0.08), (130.0, 0.04)) for fk in f])
+    save("steering.npz", f=f, sv=sv.reshape(3, len(f), 2))
+
+    with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
+        json.dump(manifest, fh, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
