@@ -1,0 +1,121 @@
+/* avz.h — C ABI of the MI355X-native mask-driven MVDR engine (libavz.so).
+ *
+ * The reference (Senpai-sama06/real-time-audio-visual-zooming) is pure Python and
+ * binds no FFI; its operator surface for this path is a set of module-level
+ * functions. Each entry point below states the reference interface it replaces
+ * (paths relative to the reference root). Host code reaches it through ctypes
+ * (real-time-audio-visual-zooming_amd/avz/_lib.py); see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only. Array pointers are DEVICE pointers (HBM),
+ *    caller-owned; strides are in elements. No allocation on the hot call.
+ *  - Every function returns 0 on success or a negative AVZ_ERR_* code and never
+ *    throws across the ABI (the reference reports errors by print-and-return,
+ *    e.g. oracle_debug.py:31-33; singular solves fall back to w = [1, 0],
+ *    oracle_debug.py:78-79 — the kernels reproduce that fallback per bin).
+ *  - A plan is immutable after creation and may be used from several streams.
+ */
+#ifndef AVZ_H_
+#define AVZ_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVZ_OK 0
+#define AVZ_ERR_ARG (-1)         /* null/invalid argument                       */
+#define AVZ_ERR_SHAPE (-2)       /* length/stride/batch outside the plan        */
+#define AVZ_ERR_HIP (-3)         /* HIP runtime error (launch / allocation)     */
+#define AVZ_ERR_UNSUPPORTED (-4) /* configuration not implemented              */
+#define AVZ_ERR_ALIGN (-5)       /* output/stride not 16-byte aligned           */
+
+/* mask sources */
+#define AVZ_MASK_IBM 0      /* oracle ideal binary mask from refs, oracle_debug.py:49-53  */
+#define AVZ_MASK_IPD 1      /* heuristic phase mask, masked_mvdr.py:37-46                 */
+#define AVZ_MASK_EXTERNAL 2 /* caller-provided target probability M, noise = 1 - M,
+                               full_audio_generating_pipeline/inference.py:99-106          */
+
+/* post-filters (A10) */
+#define AVZ_PF_NONE 0       /* masked_mvdr.py: none                                      */
+#define AVZ_PF_IBM_TARGET 1 /* x (1 - mask_noise), oracle_debug.py:84-90                 */
+#define AVZ_PF_EXT_FLOOR 2  /* x max(M, floor), full_audio.../inference.py:116           */
+#define AVZ_PF_EXT_MUL 3    /* x M, Final_pipeline/src/inference.py:219                  */
+
+/* output normalisation (A12) */
+#define AVZ_NORM_NONE 0     /* un-normalised; peak[] reports max|out|                     */
+#define AVZ_NORM_PEAK 1     /* out /= (max|out| + norm_eps), oracle_debug.py:94 (eps 0),
+                               masked_mvdr.py:128 (eps 1e-6)                              */
+
+typedef struct avz_config {
+  int fs;            /* sample rate, masked_mvdr.py:9 (16000)                         */
+  int n_fft;         /* 512 (rt_av_zoom core) or 1024 (Final_pipeline/config.py:15)   */
+  int hop;           /* must be n_fft/2 (every reference call site uses 50% overlap)  */
+  double sigma;      /* diagonal loading: 1 (oracle_debug.py:24), 1e-7, 1e-5          */
+  double angle_deg;  /* target direction, 90 (masked_mvdr.py:12)                     */
+  double mic_d;      /* mic spacing in m: 0.01 (masked_mvdr.py:10), 0.04, 0.08        */
+  double c_sound;    /* 343 (masked_mvdr.py:11)                                      */
+  double fmin_hz;    /* bins with f < fmin get w = 0 (oracle_debug.py:67: 100)       */
+  int mask_mode;     /* AVZ_MASK_*                                                   */
+  int postfilter;    /* AVZ_PF_*                                                     */
+  double pf_floor;   /* floor for AVZ_PF_EXT_FLOOR (0.05)                           */
+  double weight_eps; /* covariance weight sqrt(m + eps)^2: 0, or 1e-10 as in
+                        tf_lite_version/inference.py:109                            */
+  int normalize;     /* AVZ_NORM_*                                                   */
+  double norm_eps;   /* 0 (oracle_debug), 1e-6 (masked_mvdr), 1e-9 (oracle_reverb)   */
+  int max_batch;     /* utterances per call                                          */
+  int max_samples;   /* longest utterance (samples)                                  */
+} avz_config;
+
+typedef struct avz_plan avz_plan;
+
+/* Fused batch call. Replaces, per utterance b, the body of
+ * rt_av_zoom/core/oracle_debug.py:42-94 (IBM), rt_av_zoom/core/masked_mvdr.py:76-128
+ * (IPD) and full_audio_generating_pipeline/inference.py:88-118 (external mask):
+ * STFT -> mask -> masked covariance -> MVDR solve -> apply + post-filter -> iSTFT
+ * (-> peak normalise). out[b] has (ceil(len[b]/hop)) * hop samples
+ * (scipy.signal.istft length). */
+typedef struct avz_batch_args {
+  int batch;
+  const int* len;          /* [batch] samples per utterance (device), n_fft <= len <= max_samples */
+  int max_len;             /* host-side upper bound of len[] (validated against strides)         */
+  const float* mix;        /* [batch][2][ch_stride]: mic channels planar (y_mix [2,S])          */
+  long long mix_stride;    /* elements between utterances                                       */
+  long long ch_stride;     /* elements between the two mic channels                             */
+  const float* ref_tgt;    /* [batch][ref_stride] target reference (IBM) or NULL                */
+  const float* ref_int;    /* [batch][ref_stride] interference reference (IBM) or NULL          */
+  long long ref_stride;
+  const float* ext_mask;   /* target probability M[b][k][t] (EXTERNAL) or NULL                   */
+  long long mask_stride_b, mask_stride_f, mask_stride_t;
+  float* out;              /* [batch][out_stride], out_stride % 4 == 0, 16-byte aligned          */
+  long long out_stride;
+  float* peak;             /* [batch] max|out| before normalisation, or NULL                    */
+  double* cov_out;         /* debug: [batch][F][5] sum m|y0|^2, sum m|y1|^2, Re/Im sum m y0 y1*,
+                              sum m   (or NULL)                                                  */
+  float* w_out;            /* debug: [batch][F][4] Re w0, Im w0, Re w1, Im w1 (or NULL)         */
+} avz_batch_args;
+
+int avz_plan_create(avz_plan** plan, const avz_config* cfg);
+int avz_plan_destroy(avz_plan* plan);
+int avz_plan_get_config(const avz_plan* plan, avz_config* cfg);
+/* Frames of an utterance of len samples: ceil(len/hop) + 1 (scipy padded/boundary). */
+int avz_num_frames(const avz_plan* plan, int len);
+int avz_mvdr_batch(const avz_plan* plan, const avz_batch_args* args, void* hip_stream);
+
+/* Stage API: STFT of [batch][channels][x_stride] real signals into complex64
+ * Y[b][c][k][t] (interleaved re/im floats) with element strides; replaces the
+ * reference's scipy.signal.stft(x, fs, nperseg=n_fft, noverlap=n_fft/2) calls
+ * (oracle_debug.py:42-44, masked_mvdr.py:76, Final_pipeline/src/inference.py:198). */
+int avz_stft(const avz_plan* plan, int batch, int channels, const int* len, int max_len,
+             const float* x, long long x_stride, long long ch_stride, float* Y,
+             long long y_stride_b, long long y_stride_c, long long y_stride_f,
+             void* hip_stream);
+
+const char* avz_strerror(int code);
+/* Last HIP error string recorded by the library on this thread (diagnostics). */
+const char* avz_last_hip_error(void);
+int avz_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AVZ_H_ */

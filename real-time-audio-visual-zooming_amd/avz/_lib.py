@@ -1,0 +1,90 @@
+"""ctypes binding of libavz.so (include/avz.h). Fails loudly when the library is missing.
+
+There is no CPU fallback anywhere in ``avz``: if the HIP library cannot be loaded
+the import of this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("AVZ_LIB", os.path.join(_HERE, "libavz.so"))
+
+AVZ_OK = 0
+AVZ_ERR_ARG = -1
+AVZ_ERR_SHAPE = -2
+AVZ_ERR_HIP = -3
+AVZ_ERR_UNSUPPORTED = -4
+AVZ_ERR_ALIGN = -5
+
+MASK_IBM, MASK_IPD, MASK_EXTERNAL = 0, 1, 2
+PF_NONE, PF_IBM_TARGET, PF_EXT_FLOOR, PF_EXT_MUL = 0, 1, 2, 3
+NORM_NONE, NORM_PEAK = 0, 1
+
+EXPORTED = [
+    "avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
+    "avz_mvdr_batch", "avz_stft", "avz_strerror", "avz_last_hip_error", "avz_version",
+]
+
+
+class AvzConfig(ct.Structure):
+    _fields_ = [
+        ("fs", ct.c_int), ("n_fft", ct.c_int), ("hop", ct.c_int),
+        ("sigma", ct.c_double), ("angle_deg", ct.c_double), ("mic_d", ct.c_double),
+        ("c_sound", ct.c_double), ("fmin_hz", ct.c_double),
+        ("mask_mode", ct.c_int), ("postfilter", ct.c_int),
+        ("pf_floor", ct.c_double), ("weight_eps", ct.c_double),
+        ("normalize", ct.c_int), ("norm_eps", ct.c_double),
+        ("max_batch", ct.c_int), ("max_samples", ct.c_int),
+    ]
+
+
+class AvzBatchArgs(ct.Structure):
+    _fields_ = [
+        ("batch", ct.c_int), ("len", ct.c_void_p), ("max_len", ct.c_int),
+        ("mix", ct.c_void_p), ("mix_stride", ct.c_longlong), ("ch_stride", ct.c_longlong),
+        ("ref_tgt", ct.c_void_p), ("ref_int", ct.c_void_p), ("ref_stride", ct.c_longlong),
+        ("ext_mask", ct.c_void_p), ("mask_stride_b", ct.c_longlong),
+        ("mask_stride_f", ct.c_longlong), ("mask_stride_t", ct.c_longlong),
+        ("out", ct.c_void_p), ("out_stride", ct.c_longlong), ("peak", ct.c_void_p),
+        ("cov_out", ct.c_void_p), ("w_out", ct.c_void_p),
+    ]
+
+
+class AvzError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libavz.so not found at {LIB_PATH}; run __graft_entry__.build() "
+                          "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = ct.CDLL(LIB_PATH)
+    P = ct.c_void_p
+    lib.avz_plan_create.argtypes = [ct.POINTER(P), ct.POINTER(AvzConfig)]
+    lib.avz_plan_destroy.argtypes = [P]
+    lib.avz_plan_get_config.argtypes = [P, ct.POINTER(AvzConfig)]
+    lib.avz_num_frames.argtypes = [P, ct.c_int]
+    lib.avz_mvdr_batch.argtypes = [P, ct.POINTER(AvzBatchArgs), P]
+    lib.avz_stft.argtypes = [P, ct.c_int, ct.c_int, P, ct.c_int, P, ct.c_longlong, ct.c_longlong,
+                             P, ct.c_longlong, ct.c_longlong, ct.c_longlong, P]
+    lib.avz_strerror.argtypes = [ct.c_int]
+    lib.avz_strerror.restype = ct.c_char_p
+    lib.avz_last_hip_error.restype = ct.c_char_p
+    for name in ("avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
+                 "avz_mvdr_batch", "avz_stft", "avz_version"):
+        getattr(lib, name).restype = ct.c_int
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        msg = lib.avz_strerror(rc).decode()
+        if rc == AVZ_ERR_HIP:
+            msg += ": " + lib.avz_last_hip_error().decode()
+        raise AvzError(f"{what} failed ({rc}): {msg}")
+    return rc

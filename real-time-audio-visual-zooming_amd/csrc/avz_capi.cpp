@@ -1,0 +1,182 @@
+// avz_capi.cpp — plan management, validation and dispatch behind include/avz.h.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/avz.h"
+#include "avz_internal.h"
+
+struct avz_plan {
+  avz_config cfg;
+  double tau1, tau2;         // far-field delays of the two mics (masked_mvdr.py:28-29)
+  int max_frames;
+  uint8_t* maskbits;         // [max_batch][ceil(max_frames/4)][F] IBM nibbles
+  long long mb_stride;
+};
+
+static thread_local std::string g_last_hip;
+
+static int hip_fail(hipError_t e) {
+  g_last_hip = hipGetErrorString(e);
+  return AVZ_ERR_HIP;
+}
+
+extern "C" int avz_version(void) { return 1; }
+
+extern "C" const char* avz_last_hip_error(void) { return g_last_hip.c_str(); }
+
+extern "C" const char* avz_strerror(int code) {
+  switch (code) {
+    case AVZ_OK: return "ok";
+    case AVZ_ERR_ARG: return "invalid argument";
+    case AVZ_ERR_SHAPE: return "length, stride or batch outside the plan";
+    case AVZ_ERR_HIP: return "HIP runtime error";
+    case AVZ_ERR_UNSUPPORTED: return "unsupported configuration";
+    case AVZ_ERR_ALIGN: return "output pointer/stride not 16-byte aligned";
+    default: return "unknown error";
+  }
+}
+
+static int frames_for(int len, int hop) { return (len + hop - 1) / hop + 1; }
+
+extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
+  if (!out || !cfg) return AVZ_ERR_ARG;
+  *out = nullptr;
+  const avz_config& c = *cfg;
+  if (c.n_fft != 512 && c.n_fft != 1024) return AVZ_ERR_UNSUPPORTED;
+  if (c.hop != c.n_fft / 2) return AVZ_ERR_UNSUPPORTED;
+  if (c.fs <= 0 || c.c_sound <= 0 || !(c.sigma >= 0) || c.max_batch <= 0 ||
+      c.max_samples < c.n_fft)
+    return AVZ_ERR_ARG;
+  if (c.mask_mode < AVZ_MASK_IBM || c.mask_mode > AVZ_MASK_EXTERNAL) return AVZ_ERR_ARG;
+  if (c.postfilter < AVZ_PF_NONE || c.postfilter > AVZ_PF_EXT_MUL) return AVZ_ERR_ARG;
+  if (c.postfilter == AVZ_PF_IBM_TARGET && c.mask_mode != AVZ_MASK_IBM) return AVZ_ERR_ARG;
+  if ((c.postfilter == AVZ_PF_EXT_FLOOR || c.postfilter == AVZ_PF_EXT_MUL) &&
+      c.mask_mode != AVZ_MASK_EXTERNAL)
+    return AVZ_ERR_ARG;
+  if (c.normalize != AVZ_NORM_NONE && c.normalize != AVZ_NORM_PEAK) return AVZ_ERR_ARG;
+
+  avz_plan* p = new (std::nothrow) avz_plan();
+  if (!p) return AVZ_ERR_ARG;
+  p->cfg = c;
+  // masked_mvdr.py:22-35: tau_m1 = (d/2) cos(phi) cos(theta - 0)/c, tau_m2 with theta - pi
+  const double theta = c.angle_deg * (M_PI / 180.0);  // np.deg2rad
+  p->tau1 = (c.mic_d / 2) * std::cos(0.0) * std::cos(theta - 0) / c.c_sound;
+  p->tau2 = (c.mic_d / 2) * std::cos(0.0) * std::cos(theta - M_PI) / c.c_sound;
+  p->max_frames = frames_for(c.max_samples, c.hop);
+  const int F = c.n_fft / 2 + 1;
+  p->mb_stride = (long long)((p->max_frames + 3) / 4 + 1) * F;
+  p->maskbits = nullptr;
+  if (c.mask_mode == AVZ_MASK_IBM) {
+    hipError_t e = hipMalloc((void**)&p->maskbits, (size_t)p->mb_stride * c.max_batch);
+    if (e != hipSuccess) {
+      delete p;
+      return hip_fail(e);
+    }
+  }
+  *out = p;
+  return AVZ_OK;
+}
+
+extern "C" int avz_plan_destroy(avz_plan* p) {
+  if (!p) return AVZ_ERR_ARG;
+  if (p->maskbits) (void)hipFree(p->maskbits);
+  delete p;
+  return AVZ_OK;
+}
+
+extern "C" int avz_plan_get_config(const avz_plan* p, avz_config* cfg) {
+  if (!p || !cfg) return AVZ_ERR_ARG;
+  *cfg = p->cfg;
+  return AVZ_OK;
+}
+
+extern "C" int avz_num_frames(const avz_plan* p, int len) {
+  if (!p || len < p->cfg.n_fft) return AVZ_ERR_SHAPE;
+  return frames_for(len, p->cfg.hop);
+}
+
+extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* stream) {
+  if (!p || !a) return AVZ_ERR_ARG;
+  const avz_config& c = p->cfg;
+  if (a->batch < 0 || a->batch > c.max_batch) return AVZ_ERR_SHAPE;
+  if (a->batch == 0) return AVZ_OK;
+  if (!a->len || !a->mix || !a->out) return AVZ_ERR_ARG;
+  if (a->max_len < c.n_fft || a->max_len > c.max_samples) return AVZ_ERR_SHAPE;
+  if (a->ch_stride < a->max_len) return AVZ_ERR_SHAPE;
+  if (a->batch > 1 && a->mix_stride < a->ch_stride + a->max_len) return AVZ_ERR_SHAPE;
+  const int T = frames_for(a->max_len, c.hop);
+  const long long out_len = (long long)(T - 1) * c.hop;
+  if (a->batch > 1 && a->out_stride < out_len) return AVZ_ERR_SHAPE;
+  if ((a->out_stride & 3) || (reinterpret_cast<uintptr_t>(a->out) & 15)) return AVZ_ERR_ALIGN;
+  if (c.mask_mode == AVZ_MASK_IBM) {
+    if (!a->ref_tgt || !a->ref_int) return AVZ_ERR_ARG;
+    if (a->batch > 1 && a->ref_stride < a->max_len) return AVZ_ERR_SHAPE;
+  }
+  if (c.mask_mode == AVZ_MASK_EXTERNAL && !a->ext_mask) return AVZ_ERR_ARG;
+
+  avz::FusedArgs k{};
+  k.batch = a->batch;
+  k.len = a->len;
+  k.mix = a->mix;
+  k.mix_stride = a->mix_stride;
+  k.ch_stride = a->ch_stride;
+  k.ref_tgt = a->ref_tgt;
+  k.ref_int = a->ref_int;
+  k.ref_stride = a->ref_stride;
+  k.ext_mask = a->ext_mask;
+  k.mask_sb = a->mask_stride_b;
+  k.mask_sf = a->mask_stride_f;
+  k.mask_st = a->mask_stride_t;
+  k.out = a->out;
+  k.out_stride = a->out_stride;
+  k.peak = a->peak;
+  k.cov_out = a->cov_out;
+  k.w_out = a->w_out;
+  k.maskbits = p->maskbits;
+  k.mb_stride = p->mb_stride;
+  k.fs = c.fs;
+  k.sigma = c.sigma;
+  k.tau1 = p->tau1;
+  k.tau2 = p->tau2;
+  k.fmin_hz = c.fmin_hz;
+  k.weight_eps = (float)c.weight_eps;
+  k.pf_floor = (float)c.pf_floor;
+  k.norm_eps = (float)c.norm_eps;
+  k.postfilter = c.postfilter;
+  k.normalize = c.normalize;
+  const int rc = avz_launch_fused(c.n_fft, c.mask_mode, &k, stream);
+  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  return rc;
+}
+
+extern "C" int avz_stft(const avz_plan* p, int batch, int channels, const int* len, int max_len,
+                        const float* x, long long x_stride, long long ch_stride, float* Y,
+                        long long y_stride_b, long long y_stride_c, long long y_stride_f,
+                        void* stream) {
+  if (!p || !len || !x || !Y) return AVZ_ERR_ARG;
+  if (channels != 1 && channels != 2) return AVZ_ERR_ARG;
+  if (batch < 0) return AVZ_ERR_SHAPE;
+  if (batch == 0) return AVZ_OK;
+  if (max_len < p->cfg.n_fft) return AVZ_ERR_SHAPE;
+  const int T = frames_for(max_len, p->cfg.hop);
+  if (y_stride_f < T) return AVZ_ERR_SHAPE;
+  avz::StftArgs s{};
+  s.batch = batch;
+  s.channels = channels;
+  s.len = len;
+  s.x = x;
+  s.x_stride = x_stride;
+  s.ch_stride = ch_stride;
+  s.Y = Y;
+  s.y_stride_b = y_stride_b;
+  s.y_stride_c = y_stride_c;
+  s.y_stride_f = y_stride_f;
+  s.max_frames = T;
+  const int rc = avz_launch_stft(p->cfg.n_fft, &s, stream);
+  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  return rc;
+}

@@ -1,0 +1,236 @@
+// avz_fft.hpp — wave-level complex FFTs for gfx950 (CDNA4, wave64).
+//
+// Both transforms hold 16 complex points per lane and use exactly ONE LDS
+// transpose:
+//
+//  Fft1024   : one 1024-point FFT per wave.  N = 32 (n1) x 32 (l).
+//              step 1: 32-pt DFT over n1 = 2r + h  -> 16-pt DFT in registers per
+//                      lane half + one cross-half radix-2 (v_permlane32_swap);
+//              twiddle W1024^{l k1}; LDS transpose (32 x 33 float2, conflict-free);
+//              step 2: same 32-pt structure over l.
+//              in : lane L, reg r  <->  x[64 r + L]
+//              out: lane (k1 = L&31, h = L>>5), reg k'  <->  X[k1 + 32 k' + 512 h]
+//
+//  Fft512x2  : two independent 512-point FFTs per wave (lane group g = L>>5).
+//              N = 16 (n1, registers) x 32 (j, lanes).
+//              step 1: 16-pt DFT in registers; twiddle W512^{j k1};
+//              LDS transpose (16 x 34 float2 per group, conflict-free);
+//              step 2: 32-pt DFT over j = 2r + h: 16-pt in registers + cross-half
+//                      radix-2 between lanes 16 apart (v_permlane16_swap).
+//              in : lane (j = L&31, g), reg r  <->  x_g[j + 32 r]
+//              out: lane (k1 = L&15, h = (L>>4)&1, g), reg k'  <->  X_g[k1 + 16 k' + 256 h]
+//
+// Forward convention X[k] = sum_n x[n] exp(-2 pi i n k / N). The inverse is taken
+// as conj(FFT(conj(.))) by the callers (unnormalised).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <utility>
+
+namespace avz {
+
+struct cf {
+  float x, y;
+};
+
+__device__ __forceinline__ cf c_add(cf a, cf b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cf c_sub(cf a, cf b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cf c_mul(cf a, cf b) {
+  return {fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x)};
+}
+__device__ __forceinline__ cf c_conj(cf a) { return {a.x, -a.y}; }
+__device__ __forceinline__ cf c_scale(cf a, float s) { return {a.x * s, a.y * s}; }
+
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// W32^j = exp(-2 pi i j / 32), j in [0, 32): cos and -sin (exact zeros where exact).
+struct W32 {
+  static constexpr float c[32] = {
+      1.0f, 9.807852804e-01f, 9.238795325e-01f, 8.314696123e-01f, 7.071067812e-01f,
+      5.555702330e-01f, 3.826834324e-01f, 1.950903220e-01f, 0.0f, -1.950903220e-01f,
+      -3.826834324e-01f, -5.555702330e-01f, -7.071067812e-01f, -8.314696123e-01f,
+      -9.238795325e-01f, -9.807852804e-01f, -1.0f, -9.807852804e-01f, -9.238795325e-01f,
+      -8.314696123e-01f, -7.071067812e-01f, -5.555702330e-01f, -3.826834324e-01f,
+      -1.950903220e-01f, 0.0f, 1.950903220e-01f, 3.826834324e-01f, 5.555702330e-01f,
+      7.071067812e-01f, 8.314696123e-01f, 9.238795325e-01f, 9.807852804e-01f};
+  // s = -sin(2 pi j / 32)
+  static constexpr float s[32] = {
+      0.0f, -1.950903220e-01f, -3.826834324e-01f, -5.555702330e-01f, -7.071067812e-01f,
+      -8.314696123e-01f, -9.238795325e-01f, -9.807852804e-01f, -1.0f, -9.807852804e-01f,
+      -9.238795325e-01f, -8.314696123e-01f, -7.071067812e-01f, -5.555702330e-01f,
+      -3.826834324e-01f, -1.950903220e-01f, 0.0f, 1.950903220e-01f, 3.826834324e-01f,
+      5.555702330e-01f, 7.071067812e-01f, 8.314696123e-01f, 9.238795325e-01f,
+      9.807852804e-01f, 1.0f, 9.807852804e-01f, 9.238795325e-01f, 8.314696123e-01f,
+      7.071067812e-01f, 5.555702330e-01f, 3.826834324e-01f, 1.950903220e-01f};
+};
+
+// v * W32^J with trivial factors folded at compile time.
+template <int J>
+__device__ __forceinline__ cf w32mul(cf v) {
+  constexpr int j = ((J % 32) + 32) % 32;
+  if constexpr (j == 0) {
+    return v;
+  } else if constexpr (j == 8) {
+    return {v.y, -v.x};  // * (-i)
+  } else if constexpr (j == 16) {
+    return {-v.x, -v.y};
+  } else if constexpr (j == 24) {
+    return {-v.y, v.x};  // * (+i)
+  } else {
+    constexpr float c = W32::c[j];
+    constexpr float s = W32::s[j];
+    return {fmaf(v.x, c, -v.y * s), fmaf(v.x, s, v.y * c)};
+  }
+}
+
+// In-place forward 4-point DFT.
+__device__ __forceinline__ void dft4(cf& a0, cf& a1, cf& a2, cf& a3) {
+  const cf t0 = c_add(a0, a2), t1 = c_sub(a0, a2);
+  const cf t2 = c_add(a1, a3), t3 = c_sub(a1, a3);
+  a0 = c_add(t0, t2);
+  a2 = c_sub(t0, t2);
+  a1 = {t1.x + t3.y, t1.y - t3.x};  // t1 - i t3
+  a3 = {t1.x - t3.y, t1.y + t3.x};  // t1 + i t3
+}
+
+// In-place forward 16-point DFT on registers, natural-order output (4 x 4).
+__device__ __forceinline__ void dft16(cf (&v)[16]) {
+  static_for<0, 4>([&](auto n2) { dft4(v[n2], v[n2 + 4], v[n2 + 8], v[n2 + 12]); });
+  // v[n2 + 4 k1] = B[n2][k1]; twiddle W16^{n2 k1} = W32^{2 n2 k1}
+  static_for<1, 4>([&](auto n2) {
+    static_for<1, 4>([&](auto k1) {
+      constexpr int idx = n2 + 4 * k1;
+      v[idx] = w32mul<2 * n2 * k1>(v[idx]);
+    });
+  });
+  // 4-point DFTs over n2 (4 x 4 transpose: v[4 k1 + n2] is B[n2][k1])
+  cf t[16];
+  static_for<0, 4>([&](auto k1) {
+    // B[n2][k1] lives at v[n2 + 4 k1]; DFT along n2 for fixed k1
+    cf a0 = v[0 + 4 * k1], a1 = v[1 + 4 * k1], a2 = v[2 + 4 * k1], a3 = v[3 + 4 * k1];
+    dft4(a0, a1, a2, a3);
+    t[k1 + 0] = a0;   // X[k1 + 4 k2]
+    t[k1 + 4] = a1;
+    t[k1 + 8] = a2;
+    t[k1 + 12] = a3;
+  });
+  static_for<0, 16>([&](auto i) { v[i] = t[i]; });
+}
+
+// Cross-lane exchange between the two halves of a lane pair at distance DIST
+// (32: lanes l / l+32 via v_permlane32_swap; 16: rows 2g / 2g+1 via
+// v_permlane16_swap). Returns (value of the lower partner, value of the upper).
+template <int DIST>
+__device__ __forceinline__ void xhalf(float v, float& lo, float& hi) {
+  const unsigned u = __float_as_uint(v);
+  if constexpr (DIST == 32) {
+    auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    lo = __uint_as_float(r[0]);
+    hi = __uint_as_float(r[1]);
+  } else {
+    static_assert(DIST == 16, "DIST must be 16 or 32");
+    auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    lo = __uint_as_float(r[0]);
+    hi = __uint_as_float(r[1]);
+  }
+}
+
+// Radix-2 DIT butterfly across lane halves after both halves ran dft16 on their
+// even (h=0) / odd (h=1) inputs: out[k'] = E[k'] + sgn * W32^{k'} O[k'],
+// sgn = +1 on the lower half (bin k'), -1 on the upper half (bin k'+16).
+template <int DIST>
+__device__ __forceinline__ void xhalf_dit(cf (&v)[16], float sgn) {
+  static_for<0, 16>([&](auto k) {
+    float ex, ox, ey, oy;
+    xhalf<DIST>(v[k].x, ex, ox);
+    xhalf<DIST>(v[k].y, ey, oy);
+    const cf t = w32mul<k>(cf{ox, oy});
+    v[k] = {fmaf(sgn, t.x, ex), fmaf(sgn, t.y, ey)};
+  });
+}
+
+__device__ __forceinline__ cf unit_root(double frac) {
+  // exp(-2 pi i frac), evaluated in fp64 then rounded
+  double s, c;
+  sincospi(2.0 * frac, &s, &c);
+  return {(float)c, (float)(-s)};
+}
+
+// -------------------------------------------------------------------- Fft1024
+struct Fft1024 {
+  static constexpr int N = 1024;
+  static constexpr int SCRATCH_F2 = 32 * 33;  // float2 elements of LDS scratch
+  cf P[4], Q[4];  // W^{l j} (j<4), W^{l (4 i + 16 h)} (i<4)
+  float sgn;
+  int l, h;
+
+  __device__ __forceinline__ void init(int lane) {
+    l = lane & 31;
+    h = lane >> 5;
+    sgn = h ? -1.0f : 1.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) P[j] = unit_root((double)(l * j) / N);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Q[i] = unit_root((double)(l * (4 * i + 16 * h)) / N);
+  }
+
+  // v: x[64 r + lane] in; X[k1 + 32 r + 512 h] out. scratch: this wave's LDS slot.
+  __device__ __forceinline__ void forward(cf (&v)[16], cf* scratch) const {
+    dft16(v);
+    xhalf_dit<32>(v, sgn);
+    // reg k' holds A[l][k1 = k' + 16 h]; twiddle W1024^{l k1}
+    static_for<0, 16>([&](auto k) {
+      const cf tw = ((k & 3) == 0) ? Q[k >> 2] : c_mul(P[k & 3], Q[k >> 2]);
+      v[k] = c_mul(v[k], tw);
+    });
+    static_for<0, 16>([&](auto k) { scratch[(k + 16 * h) * 33 + l] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = scratch[l * 33 + 2 * r + h]; });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<32>(v, sgn);
+  }
+};
+
+// -------------------------------------------------------------------- Fft512x2
+struct Fft512x2 {
+  static constexpr int N = 512;
+  static constexpr int SCRATCH_F2 = 16 * 34;  // per group
+  cf P[4], Q[4];  // W512^{j i}, W512^{4 j i}
+  float sgn;      // step-2 half: (lane >> 4) & 1
+  int j, k1, h2;
+
+  __device__ __forceinline__ void init(int lane) {
+    j = lane & 31;
+    k1 = lane & 15;
+    h2 = (lane >> 4) & 1;
+    sgn = h2 ? -1.0f : 1.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) P[i] = unit_root((double)(j * i) / N);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Q[i] = unit_root((double)(4 * j * i) / N);
+  }
+
+  // v: x_g[j + 32 r] in; X_g[k1 + 16 r + 256 h] out. scratch: this lane group's slot.
+  __device__ __forceinline__ void forward(cf (&v)[16], cf* scratch) const {
+    dft16(v);  // reg k holds A[j][k]
+    static_for<1, 16>([&](auto k) {
+      const cf tw = ((k & 3) == 0) ? Q[k >> 2] : c_mul(P[k & 3], Q[k >> 2]);
+      v[k] = c_mul(v[k], tw);
+    });
+    static_for<0, 16>([&](auto k) { scratch[k * 34 + j] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = scratch[k1 * 34 + 2 * r + h2]; });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<16>(v, sgn);
+  }
+};
+
+}  // namespace avz

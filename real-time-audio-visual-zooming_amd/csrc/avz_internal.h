@@ -1,0 +1,51 @@
+// avz_internal.h — host/device shared argument blocks (not part of the public ABI).
+#pragma once
+#include <stdint.h>
+
+namespace avz {
+
+enum : int { MASK_IBM = 0, MASK_IPD = 1, MASK_EXTERNAL = 2 };
+enum : int { PF_NONE = 0, PF_IBM_TARGET = 1, PF_EXT_FLOOR = 2, PF_EXT_MUL = 3 };
+enum : int { NORM_NONE = 0, NORM_PEAK = 1 };
+
+// Everything the fused kernel needs, passed by value.
+struct FusedArgs {
+  int batch;
+  const int* len;             // [B] samples per utterance (device)
+  const float* mix;           // [B][2][..] planar
+  long long mix_stride;       // floats between utterances
+  long long ch_stride;        // floats between the two mic channels
+  const float* ref_tgt;       // [B][..] or null
+  const float* ref_int;       // [B][..] or null
+  long long ref_stride;
+  const float* ext_mask;      // target-probability mask M[b][k][t] or null
+  long long mask_sb, mask_sf, mask_st;
+  float* out;                 // [B][out_stride]
+  long long out_stride;
+  float* peak;                // [B] or null: max|out| before normalisation
+  double* cov_out;            // [B][F][5] or null: sum m|y0|^2, sum m|y1|^2, Re/Im sum m y0 y1*, sum m
+  float* w_out;               // [B][F][4] or null: Re w0, Im w0, Re w1, Im w1
+  uint8_t* maskbits;          // workspace, [B][ceil(T/4)][F] nibbles (IBM post-filter)
+  long long mb_stride;        // bytes between utterances
+  double fs, sigma, tau1, tau2, fmin_hz;
+  float weight_eps, pf_floor, norm_eps;
+  int postfilter, normalize;
+};
+
+struct StftArgs {
+  int batch, channels;        // channels 1 or 2
+  const int* len;
+  const float* x;             // [B][C][..]
+  long long x_stride, ch_stride;
+  float* Y;                   // complex64 [B][C][F][t_stride] as float2
+  long long y_stride_b, y_stride_c, y_stride_f;  // in complex elements
+  int max_frames;
+};
+
+}  // namespace avz
+
+extern "C" {
+int avz_launch_fused(int n_fft, int mask_mode, const avz::FusedArgs* a, void* stream);
+int avz_launch_stft(int n_fft, const avz::StftArgs* a, void* stream);
+int avz_fused_lds_bytes(int n_fft);
+}

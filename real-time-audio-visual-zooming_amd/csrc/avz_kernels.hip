@@ -1,0 +1,736 @@
+// avz_kernels.hip — hand-written CDNA4 (gfx950) kernels for the mask-driven MVDR chain.
+//
+// avz_fused_kernel<N, MASK>: one 1024-thread workgroup owns one utterance and runs
+//   pass 1  frames -> window -> FFT (packed mic pair / packed ref pair) -> LDS
+//           thread-per-bin: separate channels, oracle IBM / IPD / external mask,
+//           masked 2x2 covariance partials (fp32 per batch, fp64 running sums)
+//   solve   per-bin fp64 closed-form 2x2 Hermitian MVDR weights (+ steering vector)
+//   pass 2  frames -> FFT again (recompute beats spilling Y to HBM) -> LDS
+//           thread-per-bin: w^H y, post-filter gain, pack two frames into one
+//           complex spectrum -> inverse FFT -> windowed overlap-add -> out
+//   peak    block max |out|, optional in-place peak normalisation.
+// Reference semantics: rt_av_zoom/core/oracle_debug.py:27-97 (IBM path),
+// rt_av_zoom/core/masked_mvdr.py:50-132 (IPD path),
+// rt_av_zoom/core/full_audio_generating_pipeline/inference.py:88-118 (external mask),
+// scipy.signal.stft/istft framing (see oracle/avz_oracle.py).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "avz_fft.hpp"
+#include "avz_internal.h"
+
+namespace avz {
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = 16;
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, long long n_floats) {
+  long long bytes = (p == nullptr || n_floats <= 0) ? 0 : n_floats * 4;
+  if (bytes > 0x7fffffffLL) bytes = 0x7fffffffLL;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ float bload(rsrc_t r, int elem) {
+  // Offsets >= the descriptor's byte length read 0: scipy's zero extension/padding.
+  // A negative index becomes the largest dword offset (always out of range) via a
+  // select, so no voffset + immediate split can depend on 32-bit wraparound.
+  const unsigned off = (elem < 0) ? 0xfffffffcu : (unsigned)elem * 4u;
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+
+// LDS-only barrier: leaves global loads (the next frame's prefetch) in flight.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int N>
+struct KCfg;
+template <>
+struct KCfg<1024> {
+  using Fft = Fft1024;
+  static constexpr int FPW = 1;              // FFTs per wave
+  static constexpr int GROUP_BYTES = 32 * 33 * 8;
+  static constexpr int WAVE_BYTES = GROUP_BYTES;
+  static constexpr int IN_STRIDE = 64;       // sample stride between registers
+  static constexpr int OUT_STRIDE = 32;      // bin/time stride between registers
+};
+template <>
+struct KCfg<512> {
+  using Fft = Fft512x2;
+  static constexpr int FPW = 2;
+  static constexpr int GROUP_BYTES = 16 * 34 * 8;
+  static constexpr int WAVE_BYTES = 2 * GROUP_BYTES;
+  static constexpr int IN_STRIDE = 32;
+  static constexpr int OUT_STRIDE = 16;
+};
+
+template <int N, int NT = kThreads>
+struct Geo {
+  using C = KCfg<N>;
+  static constexpr int NWAVE = NT / 64;
+  static constexpr int H = N / 2;
+  static constexpr int NB = N / 2;          // bins per q-row (bin N/2 rides with k = 0)
+  static constexpr int F = N / 2 + 1;
+  static constexpr int Q = NT / NB;         // frame groups in the per-bin phase
+  static constexpr int NSLOT = NWAVE * C::FPW;
+  static constexpr int SLOT_LDS = NWAVE * C::WAVE_BYTES;
+  // + double-buffered OLA carry + Nyquist-bin running sums [Q][5] fp64 + its 2 apply coefs
+  static constexpr int LDS_BYTES = SLOT_LDS + 2 * H * 4 + Q * 5 * 8 + 16;
+  static_assert(NB * 5 * 8 * Q <= SLOT_LDS, "covariance reduction must fit the slot area");
+};
+
+template <int N>
+__device__ __forceinline__ cf* slot_ptr(unsigned char* lds, int s) {
+  using C = KCfg<N>;
+  return reinterpret_cast<cf*>(lds + (s / C::FPW) * C::WAVE_BYTES + (s % C::FPW) * C::GROUP_BYTES);
+}
+
+// Per-lane geometry of the wave FFT (input sample / output index of each register).
+template <int N>
+struct LaneMap {
+  int in0;    // input index of register 0 (lane part)
+  int grp;    // lane group (N=512: which of the two FFTs; N=1024: 0)
+  int out0;   // output index of register 0
+  __device__ __forceinline__ void init(int lane) {
+    if constexpr (N == 1024) {
+      in0 = lane;
+      grp = 0;
+      out0 = (lane & 31) + 512 * (lane >> 5);
+    } else {
+      in0 = lane & 31;
+      grp = lane >> 5;
+      out0 = (lane & 15) + 256 * ((lane >> 4) & 1);
+    }
+  }
+};
+
+// a = (z + conj zp)/2, b = (z - conj zp)/(2i): split of a packed real pair.
+// Written so that a self-partnered bin (DC, Nyquist: zp == z) yields exact +0
+// imaginary parts, as pocketfft's r2c does (matters for the IPD angle test).
+__device__ __forceinline__ void split_pair(cf z, cf zp, cf& a, cf& b) {
+  a = {0.5f * (z.x + zp.x), 0.5f * (z.y - zp.y)};
+  b = {0.5f * (z.y + zp.y), 0.5f * (zp.x - z.x)};
+}
+// DC / Nyquist bins: both parts are real; imaginary parts are +0 (pocketfft r2c).
+__device__ __forceinline__ void split_self(cf z, cf& a, cf& b) {
+  a = {z.x, 0.0f};
+  b = {z.y, 0.0f};
+}
+
+// Heuristic phase mask (masked_mvdr.py:37-46): 0.01 where angle(Y0) == angle(Y1)
+// as float32, else 1.0. A cross-product test settles every bin whose angles differ
+// by far more than an fp32 ulp; the rest compare atan2f exactly.
+__device__ __forceinline__ float ipd_weight(cf a, cf b) {
+  const float cr = a.y * b.x - a.x * b.y;
+  const float n2 = (a.x * a.x + a.y * a.y) * (b.x * b.x + b.y * b.y);
+  if (cr * cr > 1e-10f * n2) return 1.0f;
+  const float pa = atan2f(a.y, a.x), pb = atan2f(b.y, b.x);
+  return (fabsf(pa - pb) > 0.0f) ? 1.0f : 0.01f;
+}
+
+struct Acc32 {
+  float c00, c11, c01r, c01i, cm;
+  __device__ __forceinline__ void zero() { c00 = c11 = c01r = c01i = cm = 0.f; }
+  __device__ __forceinline__ void add(cf x0, cf x1, float wgt, float m) {
+    c00 = fmaf(wgt, x0.x * x0.x + x0.y * x0.y, c00);
+    c11 = fmaf(wgt, x1.x * x1.x + x1.y * x1.y, c11);
+    c01r = fmaf(wgt, x0.x * x1.x + x0.y * x1.y, c01r);  // Re x0 conj(x1)
+    c01i = fmaf(wgt, x0.y * x1.x - x0.x * x1.y, c01i);  // Im x0 conj(x1)
+    cm += m;
+  }
+};
+struct Acc64 {
+  double c[5];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) c[i] = 0.0;
+  }
+  __device__ __forceinline__ void add(const Acc32& a) {
+    c[0] += (double)a.c00;
+    c[1] += (double)a.c11;
+    c[2] += (double)a.c01r;
+    c[3] += (double)a.c01i;
+    c[4] += (double)a.cm;
+  }
+};
+
+// Per-bin MVDR solve in fp64 (oracle_debug.py:66-79):
+//   w~ = (R/(sum m + 1e-6) + sigma I)^{-1} d ; w = w~ / (d^H w~ + 1e-10);
+//   singular -> w = [1, 0]; f < fmin -> w = 0.
+// Returns the pass-2 apply coefficients S = alpha Z[k] + beta conj(Z[N-k]).
+__device__ __forceinline__ void mvdr_solve(const double (&c)[5], int k, int n_fft,
+                                           const FusedArgs& A, cf& alpha, cf& beta,
+                                           float* w_dbg) {
+  double w0r = 0, w0i = 0, w1r = 0, w1i = 0;
+  const double fk = (double)k * A.fs / (double)n_fft;
+  if (!(fk < A.fmin_hz)) {
+    const double nrm = c[4] + 1e-6;
+    const double a = c[0] / nrm + A.sigma, e = c[1] / nrm + A.sigma;
+    const double br = c[2] / nrm, bi = c[3] / nrm;
+    const double det = a * e - (br * br + bi * bi);
+    if (det == 0.0 || !isfinite(det)) {
+      w0r = 1.0;
+    } else {
+      const double om = 2.0 * M_PI * fk;
+      double s1, c1, s2, c2;
+      sincos(om * A.tau1, &s1, &c1);
+      sincos(om * A.tau2, &s2, &c2);
+      const double d0r = c1, d0i = -s1, d1r = c2, d1i = -s2;
+      // w~0 = (e d0 - b d1)/det ; w~1 = (a d1 - conj(b) d0)/det
+      double t0r = e * d0r - (br * d1r - bi * d1i);
+      double t0i = e * d0i - (br * d1i + bi * d1r);
+      double t1r = a * d1r - (br * d0r + bi * d0i);
+      double t1i = a * d1i - (br * d0i - bi * d0r);
+      t0r /= det; t0i /= det; t1r /= det; t1i /= det;
+      // den = conj(d0) w~0 + conj(d1) w~1 + 1e-10
+      const double dr = d0r * t0r + d0i * t0i + d1r * t1r + d1i * t1i + 1e-10;
+      const double di = d0r * t0i - d0i * t0r + d1r * t1i - d1i * t1r;
+      const double dd = dr * dr + di * di;
+      w0r = (t0r * dr + t0i * di) / dd;
+      w0i = (t0i * dr - t0r * di) / dd;
+      w1r = (t1r * dr + t1i * di) / dd;
+      w1i = (t1i * dr - t1r * di) / dd;
+    }
+  }
+  // alpha = (conj w0 - i conj w1)/2 ; beta = (conj w0 + i conj w1)/2
+  alpha = {(float)(0.5 * (w0r - w1i)), (float)(0.5 * (-w0i - w1r))};
+  beta = {(float)(0.5 * (w0r + w1i)), (float)(0.5 * (-w0i + w1r))};
+  if (w_dbg) {
+    w_dbg[0] = (float)w0r;
+    w_dbg[1] = (float)w0i;
+    w_dbg[2] = (float)w1r;
+    w_dbg[3] = (float)w1i;
+  }
+}
+
+__device__ __forceinline__ cf apply_bin(cf alpha, cf beta, cf z, cf zp, float g) {
+  const cf s = c_add(c_mul(alpha, z), c_mul(beta, c_conj(zp)));
+  return {g * s.x, g * s.y};
+}
+
+template <int N, int MASK, int NT>
+__global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
+  using C = KCfg<N>;
+  using G = Geo<N, NT>;
+  constexpr int NWAVE = G::NWAVE;
+  constexpr int H = G::H, NB = G::NB, F = G::F, Q = G::Q, NSLOT = G::NSLOT;
+  constexpr int FB1 = (MASK == MASK_IBM) ? NSLOT / 2 : NSLOT;  // frames per pass-1 batch
+  constexpr int FPT1 = FB1 / Q;                                  // frames per thread, pass 1
+  constexpr int FB2 = NSLOT;
+  constexpr int FPT2 = FB2 / Q;
+  static_assert(MASK != MASK_IBM || FPT1 == 4, "IBM nibble layout assumes 4 frames/thread");
+  static_assert(FPT2 == 8, "pass-2 layout assumes 8 frames/thread");
+
+  extern __shared__ __align__(16) unsigned char lds[];
+  float* carry = reinterpret_cast<float*>(lds + G::SLOT_LDS);  // [2][H]
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
+  const int lane = tid & 63;
+  const int L = A.len[b];
+  if (L < N) {  // host validates; a bad device length must not fault
+    if (tid == 0 && A.peak) A.peak[b] = __builtin_nanf("");
+    return;
+  }
+  const int T = (L + H - 1) / H + 1;  // scipy: ceil(L/H) + 1 frames
+  const int NB1 = (T + FB1 - 1) / FB1, NB2 = (T + FB2 - 1) / FB2;
+  const int NSTEP = NB1 + NB2;
+
+  // ---------------- per-lane FFT state
+  typename C::Fft fft;
+  fft.init(lane);
+  LaneMap<N> lm;
+  lm.init(lane);
+  const int my_slot = wave * C::FPW + lm.grp;
+  cf* my_spec = slot_ptr<N>(lds, my_slot);
+
+  // analysis window * (1 / sum(win)): win[n] = 0.5 - 0.5 cos(2 pi n / N), n = in0 + IN_STRIDE r
+  float wa0, wac, was;
+  {
+    double s, c;
+    sincospi(2.0 * lm.in0 / N, &s, &c);
+    const double sc = 2.0 / N;
+    wa0 = (float)(0.5 * sc);
+    wac = (float)(0.5 * sc * c);
+    was = (float)(0.5 * sc * s);
+  }
+  // synthesis window * sum(win)/N for IFFT output n = out0 + OUT_STRIDE k'
+  float ws0, wsc, wss;
+  {
+    double s, c;
+    sincospi(2.0 * lm.out0 / N, &s, &c);
+    ws0 = 0.25f;
+    wsc = (float)(0.25 * c);
+    wss = (float)(0.25 * s);
+  }
+
+  // ---------------- buffer descriptors (wave-uniform)
+  const float* mixb = A.mix + (long long)b * A.mix_stride;
+  const rsrc_t r_m0 = make_rsrc(mixb, L);
+  const rsrc_t r_m1 = make_rsrc(mixb + A.ch_stride, L);
+  rsrc_t r_t = r_m0, r_i = r_m1;
+  if constexpr (MASK == MASK_IBM) {
+    r_t = make_rsrc(A.ref_tgt + (long long)b * A.ref_stride, L);
+    r_i = make_rsrc(A.ref_int + (long long)b * A.ref_stride, L);
+  }
+
+  cf v[16];
+  auto issue_loads = [&](int step) {
+    bool ref = false;
+    int frame;
+    if (step < NB1) {
+      if constexpr (MASK == MASK_IBM) {
+        ref = wave * C::FPW >= FB1;  // uniform: the whole wave transforms references
+        frame = step * FB1 + (ref ? my_slot - FB1 : my_slot);
+      } else {
+        frame = step * FB1 + my_slot;
+      }
+    } else {
+      frame = (step - NB1) * FB2 + my_slot;
+    }
+    const rsrc_t re = ref ? r_t : r_m0;
+    const rsrc_t im = ref ? r_i : r_m1;
+    const int s0 = frame * H - N / 2 + lm.in0;
+    static_for<0, 16>([&](auto r) {
+      v[r].x = bload(re, s0 + C::IN_STRIDE * r);
+      v[r].y = bload(im, s0 + C::IN_STRIDE * r);
+    });
+  };
+  auto window_and_fft = [&]() {
+    static_for<0, 16>([&](auto r) {
+      constexpr float cr = W32::c[2 * r], sr = -W32::s[2 * r];  // cos, sin of 2 pi r / 16
+      const float w = fmaf(was, sr, fmaf(-wac, cr, wa0));
+      v[r] = c_scale(v[r], w);
+    });
+    fft.forward(v, my_spec);
+    // natural-order spectrum into this lane group's slot
+    static_for<0, 16>([&](auto k) { my_spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
+  };
+
+  // ---------------- per-bin thread role
+  // Thread (kb, q) owns bin kb for the frames of row q. Bin 0 is self-partnered
+  // (kp = 0) and needs no special case; the Nyquist bin N/2 is extra work of the
+  // kb == 0 threads, with its running state kept in LDS.
+  const int kb = tid % NB;
+  const int q = tid / NB;
+  const bool nyq = (kb == 0);
+  const int kp = (N - kb) & (N - 1);
+  uint8_t* mb = A.maskbits + (long long)b * A.mb_stride;
+  double* nyq_acc = reinterpret_cast<double*>(lds + G::SLOT_LDS + 2 * H * 4);  // [Q][5]
+  cf* nyq_ab = reinterpret_cast<cf*>(nyq_acc + Q * 5);                        // alpha_n, beta_n
+  cf alpha{0, 0}, beta{0, 0};
+
+  auto bin_weight = [&](cf x0, cf x1, const cf* Zr, int k, int kk, int t, bool& noise,
+                        float& wgt) -> float {
+    float m;
+    if constexpr (MASK == MASK_IBM) {
+      const cf zr = Zr[k], zrp = Zr[kk];
+      // 2T = zr + conj(zrp), 2I = (zr - conj zrp)/i ; |2I|^2 > |2T|^2 <=> |I| > |T|
+      const float tr = zr.x + zrp.x, ti = zr.y - zrp.y;
+      const float ir = zr.y + zrp.y, ii = zr.x - zrp.x;
+      noise = ir * ir + ii * ii > tr * tr + ti * ti;
+      m = noise ? 1.0f : 0.0f;
+      wgt = m;
+    } else if constexpr (MASK == MASK_IPD) {
+      m = ipd_weight(x0, x1);
+      wgt = m;
+    } else {
+      const float M = A.ext_mask[(long long)b * A.mask_sb + (long long)k * A.mask_sf +
+                                 (long long)t * A.mask_st];
+      m = 1.0f - M;
+      wgt = m + A.weight_eps;
+    }
+    return m;
+  };
+
+  // ======================= pass 1: masks + covariance =======================
+  if (nyq) {
+#pragma unroll
+    for (int c = 0; c < 5; ++c) nyq_acc[q * 5 + c] = 0.0;
+  }
+  issue_loads(0);
+  {
+    Acc64 acc;
+    acc.zero();
+    for (int step = 0; step < NB1; ++step) {
+      window_and_fft();
+      issue_loads(step + 1);  // step NB1 is pass 2's first batch
+      lds_barrier();
+      const int f0 = step * FB1;
+      const int tq = f0 + q * FPT1;
+      Acc32 a32;
+      a32.zero();
+      unsigned nib = 0;
+#pragma unroll 1
+      for (int i = 0; i < FPT1; ++i) {
+        const int f = q * FPT1 + i;
+        if (tq + i >= T) break;
+        const cf* Zm = slot_ptr<N>(lds, f);
+        cf x0, x1;
+        split_pair(Zm[kb], Zm[kp], x0, x1);
+        bool noise = false;
+        float wgt;
+        const float m = bin_weight(x0, x1, slot_ptr<N>(lds, FB1 + f), kb, kp, tq + i, noise, wgt);
+        nib |= (noise ? 1u : 0u) << i;
+        a32.add(x0, x1, wgt, m);
+      }
+      acc.add(a32);
+      if (nyq) {  // Nyquist bin: self-partnered, running sums in LDS
+        Acc32 an;
+        an.zero();
+        unsigned nibn = 0;
+        for (int i = 0; i < FPT1; ++i) {
+          const int f = q * FPT1 + i;
+          if (tq + i >= T) break;
+          cf y0, y1;
+          const cf* Zm = slot_ptr<N>(lds, f);
+          split_pair(Zm[N / 2], Zm[N / 2], y0, y1);
+          bool noise = false;
+          float wn;
+          const float mn = bin_weight(y0, y1, slot_ptr<N>(lds, FB1 + f), N / 2, N / 2, tq + i,
+                                      noise, wn);
+          nibn |= (noise ? 1u : 0u) << i;
+          an.add(y0, y1, wn, mn);
+        }
+        nyq_acc[q * 5 + 0] += (double)an.c00;
+        nyq_acc[q * 5 + 1] += (double)an.c11;
+        nyq_acc[q * 5 + 2] += (double)an.c01r;
+        nyq_acc[q * 5 + 3] += (double)an.c01i;
+        nyq_acc[q * 5 + 4] += (double)an.cm;
+        if constexpr (MASK == MASK_IBM) {
+          if (tq < T) mb[(long long)(tq >> 2) * F + N / 2] = (uint8_t)nibn;
+        }
+      }
+      if constexpr (MASK == MASK_IBM) {
+        if (tq < T) mb[(long long)(tq >> 2) * F + kb] = (uint8_t)nib;
+      }
+      lds_barrier();
+    }
+
+    // ============ solve: reduce the Q partial rows, fp64 MVDR ============
+    double* part = reinterpret_cast<double*>(lds);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) part[(q * NB + kb) * 5 + c] = acc.c[c];
+    __syncthreads();  // also publishes the global mask nibbles to pass 2
+    double R[5] = {0, 0, 0, 0, 0};
+    for (int qq = 0; qq < Q; ++qq) {
+#pragma unroll
+      for (int c = 0; c < 5; ++c) R[c] += part[(qq * NB + kb) * 5 + c];
+    }
+    const bool dbg = (q == 0);
+    float* wdbg = (A.w_out && dbg) ? A.w_out + ((long long)b * F + kb) * 4 : nullptr;
+    mvdr_solve(R, kb, N, A, alpha, beta, wdbg);
+    if (A.cov_out && dbg) {
+#pragma unroll
+      for (int c = 0; c < 5; ++c) A.cov_out[((long long)b * F + kb) * 5 + c] = R[c];
+    }
+    if (tid == 0) {
+      double Rn[5] = {0, 0, 0, 0, 0};
+      for (int qq = 0; qq < Q; ++qq) {
+#pragma unroll
+        for (int c = 0; c < 5; ++c) Rn[c] += nyq_acc[qq * 5 + c];
+      }
+      float* wdbgn = A.w_out ? A.w_out + ((long long)b * F + N / 2) * 4 : nullptr;
+      mvdr_solve(Rn, N / 2, N, A, nyq_ab[0], nyq_ab[1], wdbgn);
+      if (A.cov_out) {
+#pragma unroll
+        for (int c = 0; c < 5; ++c) A.cov_out[((long long)b * F + N / 2) * 5 + c] = Rn[c];
+      }
+    }
+    lds_barrier();
+  }
+
+  // ============ pass 2: apply + post-filter + iSTFT overlap-add ============
+  // OLA role: 4 consecutive samples m of segments {sgrp, sgrp + NSG}
+  constexpr int M4 = N / 8;  // float4 groups per half frame
+  constexpr int NSG = NT / M4;
+  static_assert(2 * NSG == FB2, "OLA mapping");
+  const int m0 = 4 * (tid % M4);
+  const int sgrp = tid / M4;
+  float peak = 0.0f;
+  constexpr int NPAIR = FB2 / 2;
+  const bool ifft_wave = wave < NPAIR / C::FPW;
+  for (int st2 = 0; st2 < NB2; ++st2) {
+    const int step = NB1 + st2;
+    const bool more = step + 1 < NSTEP;
+    window_and_fft();
+    if (!ifft_wave && more) issue_loads(step + 1);  // idle during the inverse FFT: prefetch now
+    lds_barrier();
+
+    const int f0 = st2 * FB2;
+    const int tq = f0 + q * FPT2;
+    {
+      auto gain = [&](int i, int t, uint32_t bb, int kk) -> float {
+        if (t >= T) return 0.0f;
+        switch (A.postfilter) {
+          case PF_IBM_TARGET: return ((bb >> i) & 1u) ? 0.0f : 1.0f;
+          case PF_EXT_FLOOR:
+          case PF_EXT_MUL: {
+            const float M = A.ext_mask[(long long)b * A.mask_sb + (long long)kk * A.mask_sf +
+                                       (long long)t * A.mask_st];
+            return A.postfilter == PF_EXT_FLOOR ? fmaxf(M, A.pf_floor) : M;
+          }
+          default: return 1.0f;
+        }
+      };
+      auto load_bits = [&](int kk) -> uint32_t {  // bit i: frame tq + i is noise (IBM)
+        uint32_t bb = 0;
+        if (A.postfilter == PF_IBM_TARGET && tq < T) {
+          const uint8_t* row = mb + (long long)(tq >> 2) * F;
+          bb = row[kk];
+          if (tq + 4 < T) bb |= (uint32_t)row[F + kk] << 4;
+        }
+        return bb;
+      };
+      const uint32_t bits = load_bits(kb);
+#pragma unroll 1
+      for (int pi = 0; pi < FPT2 / 2; ++pi) {
+        const int fa = q * FPT2 + 2 * pi;
+        const int ta = tq + 2 * pi;
+        if (ta >= T) break;
+        cf* Za = slot_ptr<N>(lds, fa);
+        const cf* Zb = slot_ptr<N>(lds, fa + 1);
+        const float ga = gain(2 * pi, ta, bits, kb), gb = gain(2 * pi + 1, ta + 1, bits, kb);
+        const cf za = Za[kb], zap = Za[kp], zb = Zb[kb], zbp = Zb[kp];
+        const cf sa = apply_bin(alpha, beta, za, zap, ga);
+        const cf sb = apply_bin(alpha, beta, zb, zbp, gb);
+        Za[kp] = {sa.x + sb.y, sb.x - sa.y};  // conj(Sa) + i conj(Sb) at N - k
+        // Sa + i Sb at k; at DC irfft keeps only the real parts (written last: kp == kb)
+        Za[kb] = nyq ? cf{sa.x, sb.x} : cf{sa.x - sb.y, sa.y + sb.x};
+      }
+      if (nyq) {  // Nyquist bin
+        const uint32_t bitsn = load_bits(N / 2);
+        const cf an = nyq_ab[0], bn = nyq_ab[1];
+        for (int pi = 0; pi < FPT2 / 2; ++pi) {
+          const int fa = q * FPT2 + 2 * pi;
+          const int ta = tq + 2 * pi;
+          if (ta >= T) break;
+          cf* Za = slot_ptr<N>(lds, fa);
+          const cf* Zb = slot_ptr<N>(lds, fa + 1);
+          const float ga = gain(2 * pi, ta, bitsn, N / 2);
+          const float gb = gain(2 * pi + 1, ta + 1, bitsn, N / 2);
+          const cf za = Za[N / 2], zb = Zb[N / 2];
+          Za[N / 2] = {apply_bin(an, bn, za, za, ga).x, apply_bin(an, bn, zb, zb, gb).x};
+        }
+      }
+    }
+    lds_barrier();
+
+    // ---- inverse FFT of packed pairs -> windowed frame contributions (waves < NPAIR/FPW)
+    if (ifft_wave) {
+      const int p = wave * C::FPW + lm.grp;
+      cf* Zi = slot_ptr<N>(lds, 2 * p);
+      static_for<0, 16>([&](auto r) { v[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
+      fft.forward(v, Zi);
+      float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
+      static_for<0, 16>([&](auto k) {
+        constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+        const float w = fmaf(wss, sk, fmaf(-wsc, ck, ws0));
+        const int n = lm.out0 + C::OUT_STRIDE * k;
+        Cp[n] = v[k].x * w;       // frame 2p   (real part of the inverse)
+        Cp[N + n] = -v[k].y * w;  // frame 2p+1 (imag part; conj trick)
+      });
+      if (more) issue_loads(step + 1);
+    }
+    lds_barrier();
+
+    // ---- overlap-add: segment j = frame j (2nd half) + frame j+1 (1st half)
+    {
+      const int bsel = st2 & 1;
+      const float* cin = carry + bsel * H;
+      float* cout = carry + (bsel ^ 1) * H;
+      float* outb = A.out + (long long)b * A.out_stride;
+      auto cframe = [&](int f) -> const float* {
+        return reinterpret_cast<const float*>(slot_ptr<N>(lds, 2 * (f >> 1) + 1)) + (f & 1) * N;
+      };
+#pragma unroll
+      for (int si = 0; si < 2; ++si) {
+        const int s = sgrp + si * NSG;
+        const int j = f0 - 1 + s;
+        if (j >= 0 && j <= T - 2) {
+          const float* pa = (s == 0) ? cin + m0 : cframe(s - 1) + H + m0;
+          const float* pb = cframe(s) + m0;
+          const float4 va = *reinterpret_cast<const float4*>(pa);
+          const float4 vb = *reinterpret_cast<const float4*>(pb);
+          float in[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {  // 1 / (win[m]^2 + win[m + N/2]^2)
+            const float c1 = cospif(2.0f * (float)(m0 + i) / (float)N);
+            const float wa = 0.5f - 0.5f * c1, wb = 0.5f + 0.5f * c1;
+            in[i] = 1.0f / (wa * wa + wb * wb);
+          }
+          float4 o;
+          o.x = (va.x + vb.x) * in[0];
+          o.y = (va.y + vb.y) * in[1];
+          o.z = (va.z + vb.z) * in[2];
+          o.w = (va.w + vb.w) * in[3];
+          *reinterpret_cast<float4*>(outb + (long long)j * H + m0) = o;
+          peak = fmaxf(peak, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+        }
+      }
+      if (sgrp == 0) {
+        *reinterpret_cast<float4*>(cout + m0) =
+            *reinterpret_cast<const float4*>(cframe(FB2 - 1) + H + m0);
+      }
+    }
+    lds_barrier();
+  }
+
+  // ---------------- block max |out|, optional in-place normalisation
+  for (int o = 32; o > 0; o >>= 1) peak = fmaxf(peak, __shfl_xor(peak, o, 64));
+  float* red = reinterpret_cast<float*>(lds);
+  if (lane == 0) red[wave] = peak;
+  __syncthreads();
+  float pk = red[0];
+#pragma unroll
+  for (int w = 1; w < NWAVE; ++w) pk = fmaxf(pk, red[w]);
+  if (tid == 0 && A.peak) A.peak[b] = pk;
+  if (A.normalize == NORM_PEAK) {
+    const float scale = 1.0f / (pk + A.norm_eps);
+    float* outb = A.out + (long long)b * A.out_stride;
+    const int n4 = (T - 1) * H / 4;
+    float4* o4 = reinterpret_cast<float4*>(outb);
+    for (int i = tid; i < n4; i += NT) {
+      float4 x = o4[i];
+      x.x *= scale; x.y *= scale; x.z *= scale; x.w *= scale;
+      o4[i] = x;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Standalone STFT (stage API / parity): Y[b][c][k][t] = scipy.signal.stft(x[b][c])
+// One block per (utterance, NSLOT-frame batch); each lane group transforms one
+// frame of the packed channel pair, then threads split the pair per bin.
+template <int N>
+__global__ void __launch_bounds__(kThreads, 1) avz_stft_kernel(StftArgs A) {
+  using C = KCfg<N>;
+  using G = Geo<N>;
+  constexpr int H = G::H, F = G::F, NSLOT = G::NSLOT;
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int b = blockIdx.x;
+  const int f0 = blockIdx.y * NSLOT;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int L = A.len[b];
+  const int T = (L + H - 1) / H + 1;
+  if (f0 >= T) return;
+
+  typename C::Fft fft;
+  fft.init(lane);
+  LaneMap<N> lm;
+  lm.init(lane);
+  const int my_slot = wave * C::FPW + lm.grp;
+  cf* spec = slot_ptr<N>(lds, my_slot);
+  const float* xb = A.x + (long long)b * A.x_stride;
+  const rsrc_t re = make_rsrc(xb, L);
+  const rsrc_t im = make_rsrc(A.channels > 1 ? xb + A.ch_stride : nullptr, L);
+  float wa0, wac, was;
+  {
+    double s, c;
+    sincospi(2.0 * lm.in0 / N, &s, &c);
+    const double sc = 2.0 / N;
+    wa0 = (float)(0.5 * sc);
+    wac = (float)(0.5 * sc * c);
+    was = (float)(0.5 * sc * s);
+  }
+  cf v[16];
+  const int s0 = (f0 + my_slot) * H - N / 2 + lm.in0;
+  static_for<0, 16>([&](auto r) {
+    constexpr float cr = W32::c[2 * r], sr = -W32::s[2 * r];
+    const float w = fmaf(was, sr, fmaf(-wac, cr, wa0));
+    v[r] = {bload(re, s0 + C::IN_STRIDE * r) * w, bload(im, s0 + C::IN_STRIDE * r) * w};
+  });
+  fft.forward(v, spec);
+  static_for<0, 16>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
+  __syncthreads();
+  float2* Y = reinterpret_cast<float2*>(A.Y);
+  for (int idx = tid; idx < F * NSLOT; idx += kThreads) {
+    const int k = idx / NSLOT, f = idx % NSLOT;
+    const int t = f0 + f;
+    if (t >= T) continue;
+    const cf* Z = slot_ptr<N>(lds, f);
+    cf a, c;
+    if (k == 0 || k == N / 2) split_self(Z[k], a, c);
+    else split_pair(Z[k], Z[N - k], a, c);
+    const long long o = (long long)b * A.y_stride_b + (long long)k * A.y_stride_f + t;
+    Y[o] = make_float2(a.x, a.y);
+    if (A.channels > 1) Y[o + A.y_stride_c] = make_float2(c.x, c.y);
+  }
+}
+
+}  // namespace avz
+
+using namespace avz;
+
+#ifndef AVZ_FUSED_THREADS
+#define AVZ_FUSED_THREADS 512
+#endif
+constexpr int kFusedThreads = AVZ_FUSED_THREADS;
+
+extern "C" int avz_fused_lds_bytes(int n_fft) {
+  return n_fft == 1024 ? Geo<1024, kFusedThreads>::LDS_BYTES
+         : n_fft == 512 ? Geo<512, kFusedThreads>::LDS_BYTES : -1;
+}
+
+template <int N, int MASK>
+static int launch_fused_t(const FusedArgs* a, hipStream_t st) {
+  auto kern = avz_fused_kernel<N, MASK, kFusedThreads>;
+  const int lds = Geo<N, kFusedThreads>::LDS_BYTES;
+  static bool attr_done = false;
+  if (!attr_done) {
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+        hipSuccess)
+      return -3;
+    attr_done = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(a->batch), dim3(kFusedThreads), lds, st, *a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int avz_launch_fused(int n_fft, int mask_mode, const FusedArgs* a, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (a->batch <= 0) return 0;
+  if (n_fft == 1024) {
+    switch (mask_mode) {
+      case MASK_IBM: return launch_fused_t<1024, MASK_IBM>(a, st);
+      case MASK_IPD: return launch_fused_t<1024, MASK_IPD>(a, st);
+      case MASK_EXTERNAL: return launch_fused_t<1024, MASK_EXTERNAL>(a, st);
+    }
+  } else if (n_fft == 512) {
+    switch (mask_mode) {
+      case MASK_IBM: return launch_fused_t<512, MASK_IBM>(a, st);
+      case MASK_IPD: return launch_fused_t<512, MASK_IPD>(a, st);
+      case MASK_EXTERNAL: return launch_fused_t<512, MASK_EXTERNAL>(a, st);
+    }
+  }
+  return -4;
+}
+
+template <int N>
+static int launch_stft_t(const StftArgs* a, hipStream_t st) {
+  auto kern = avz_stft_kernel<N>;
+  const int lds = Geo<N>::SLOT_LDS;
+  static bool attr_done = false;
+  if (!attr_done) {
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+        hipSuccess)
+      return -3;
+    attr_done = true;
+  }
+  dim3 grid(a->batch, (a->max_frames + Geo<N>::NSLOT - 1) / Geo<N>::NSLOT);
+  hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, st, *a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int avz_launch_stft(int n_fft, const StftArgs* a, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (a->batch <= 0) return 0;
+  if (n_fft == 1024) return launch_stft_t<1024>(a, st);
+  if (n_fft == 512) return launch_stft_t<512>(a, st);
+  return -4;
+}

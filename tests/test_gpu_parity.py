@@ -1,0 +1,206 @@
+"""GPU parity: the HIP path (through the C ABI) against the pinned CPU oracle and the
+reference's golden vectors. Tolerances (BASELINE.md section 4 / SURVEY 8(a)):
+peak-normalised waveform max-abs <= 1e-4 and SIR |delta| <= 0.01 dB vs the reference
+on identical inputs; STFT bins within 2e-6 of max|Y| (fp32 FFT vs pocketfft)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden, triple_f32
+from oracle import avz_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+WAVE_TOL = 1e-4
+SIR_TOL = 0.01
+
+
+@pytest.fixture(scope="module")
+def avz(gpu_device):
+    import avz as _avz
+    return _avz
+
+
+def dev_t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def run_ibm(avz, dev, mix, tgt, itf, n, sigma, normalize="peak", debug=False, mic_d=0.01):
+    plan = avz.MVDRPlan(n_fft=n, sigma=sigma, mic_d=mic_d, mask="ibm", postfilter="ibm",
+                        normalize=normalize, max_batch=1, max_samples=len(tgt))
+    F = n // 2 + 1
+    cov = torch.zeros((1, F, 5), dtype=torch.float64, device=dev) if debug else None
+    w = torch.zeros((1, F, 4), dtype=torch.float32, device=dev) if debug else None
+    out, peak = plan.run(dev_t(mix, dev)[None], ref_tgt=dev_t(tgt, dev)[None],
+                         ref_int=dev_t(itf, dev)[None], cov_out=cov, w_out=w)
+    torch.cuda.synchronize()
+    n_out = plan.out_len(len(tgt))
+    res = out[0, :n_out].cpu().numpy().astype(np.float64)
+    if debug:
+        return res, float(peak[0]), cov[0].cpu().numpy(), w[0].cpu().numpy()
+    return res, float(peak[0])
+
+
+def sir(out, tgt, itf):
+    L = min(len(out), len(tgt))
+    return O.projection_sdr_sir(out[:L], tgt[:L], itf[:L])[1]
+
+
+# ----------------------------------------------------------------------------- STFT stage
+@pytest.mark.parametrize("n", [512, 1024])
+def test_stft_stage(avz, gpu_device, n):
+    rng = np.random.default_rng(n)
+    lens = [n, n + 1, 3 * n // 2 + 7, 20000]
+    S = max(lens)
+    x = np.zeros((len(lens), 2, S), np.float32)
+    for b, L in enumerate(lens):
+        x[b, :, :L] = rng.standard_normal((2, L)).astype(np.float32)
+    plan = avz.MVDRPlan(n_fft=n, mask="ipd", postfilter="none", max_batch=len(lens), max_samples=S)
+    Y = plan.stft(dev_t(x, gpu_device), torch.tensor(lens, dtype=torch.int32, device=gpu_device),
+                  max_len=S).cpu().numpy()
+    for b, L in enumerate(lens):
+        _, _, Yr = O.stft(x[b, :, :L], nperseg=n, noverlap=n // 2)
+        T = Yr.shape[-1]
+        got = Y[b, :, :, :T]
+        assert np.max(np.abs(got - Yr)) <= 2e-6 * np.max(np.abs(Yr))
+        # DC / Nyquist imaginary parts are exactly +0 (pocketfft r2c)
+        assert np.all(got[:, 0, :].imag == 0) and np.all(got[:, -1, :].imag == 0)
+        assert not np.any(np.signbit(got[:, 0, :].imag))
+
+
+# ----------------------------------------------------------------------------- fused IBM
+EXC = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "excerpt_*.npz")))
+FULL = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "full_*.npz")))
+
+
+@pytest.mark.parametrize("name", EXC)
+def test_fused_ibm_excerpt_vs_reference(avz, gpu_device, name):
+    g = golden(name)
+    trip = name.split("_")[1]
+    mix, tgt, itf = triple_f32(trip, g["seg"])
+    n, s = int(g["n_fft"]), float(g["sigma"])
+    out, peak, cov, w = run_ibm(avz, gpu_device, mix, tgt, itf, n, s, debug=True)
+    ref = g["out"].astype(np.float64)
+    assert len(out) == len(ref)
+    assert np.max(np.abs(out - ref)) <= WAVE_TOL
+    assert abs(sir(out, tgt, itf) - sir(ref, tgt, itf)) <= SIR_TOL
+    assert abs(peak - float(g["peak_raw"])) <= 1e-4 * float(g["peak_raw"])
+    # stage parity against the oracle's fp64 covariance / weights
+    _, st = O.oracle_debug_vec(mix, tgt, itf, n_fft=n, hop=n // 2, sigma=s, return_stages=True)
+    msum = st["mask"].sum(axis=1)
+    # IBM counts are exact except where |S_int| ~ |S_tgt| to fp32 rounding (the GPU STFT is
+    # fp32; scipy's is fp64 rounded to complex64): every flipped bin must hold a near tie.
+    diff = np.nonzero(cov[:, 4] != msum)[0]
+    assert len(diff) <= max(1, len(msum) // 100)
+    for k in diff:
+        a, b = np.abs(st["S_i"][k]), np.abs(st["S_t"][k])
+        rel = np.abs(a - b) / np.maximum(np.maximum(a, b), 1e-30)
+        assert np.min(rel) < 1e-5, (k, np.min(rel))
+    ok = cov[:, 4] == msum
+    R = st["R"] * (msum + 1e-6)[:, None, None]
+    scale = np.max(np.abs(R[:, 0, 0]))
+    np.testing.assert_allclose(cov[ok, 0], R[ok, 0, 0].real, atol=2e-6 * scale)
+    np.testing.assert_allclose(cov[ok, 2] + 1j * cov[ok, 3], R[ok, 0, 1], atol=2e-6 * scale)
+    W = w[:, 0] + 1j * w[:, 1], w[:, 2] + 1j * w[:, 3]
+    np.testing.assert_allclose(W[0][ok], st["W"][ok, 0], atol=1e-3 * np.max(np.abs(st["W"])))
+    np.testing.assert_allclose(W[1][ok], st["W"][ok, 1], atol=1e-3 * np.max(np.abs(st["W"])))
+
+
+@pytest.mark.parametrize("name", FULL)
+def test_fused_ibm_full_length_vs_reference(avz, gpu_device, name):
+    g = golden(name)
+    trip = name.split("_")[1]
+    mix, tgt, itf = triple_f32(trip)
+    n, s = int(g["n_fft"]), float(g["sigma"])
+    out, _ = run_ibm(avz, gpu_device, mix, tgt, itf, n, s)
+    assert len(out) == int(g["out_len"])
+    assert np.max(np.abs(out[::16] - g["out_stride16"])) <= WAVE_TOL
+    assert np.max(np.abs(out[:4096] - g["out_head"])) <= WAVE_TOL
+    assert abs(sir(out, tgt, itf) - float(g["sir_out"])) <= SIR_TOL
+    # full-array check against the oracle (identical inputs)
+    ref = O.oracle_debug_vec(mix, tgt, itf, n_fft=n, hop=n // 2, sigma=s)
+    assert np.max(np.abs(out - ref)) <= WAVE_TOL
+
+
+# ----------------------------------------------------------------------------- fused IPD
+@pytest.mark.parametrize("trip", ["test", "set2"])
+@pytest.mark.parametrize("n", [512, 1024])
+def test_fused_ipd_vs_reference(avz, gpu_device, trip, n):
+    g = golden(f"ipd_{trip}_n{n}.npz")
+    mix, tgt, itf = triple_f32(trip)
+    plan = avz.MVDRPlan(n_fft=n, sigma=1e-7, mic_d=0.01, mask="ipd", postfilter="none",
+                        normalize="peak", norm_eps=1e-6, max_batch=1, max_samples=len(tgt))
+    out, _ = plan.run(dev_t(mix, gpu_device)[None])
+    torch.cuda.synchronize()
+    out = out[0, :plan.out_len(len(tgt))].cpu().numpy().astype(np.float64)
+    assert len(out) == int(g["out_len"])
+    ref = O.masked_mvdr_vec(mix, n_fft=n, hop=n // 2)
+    assert np.max(np.abs(out - ref)) <= WAVE_TOL
+    assert np.max(np.abs(out[::16] - g["out_stride16"])) <= WAVE_TOL
+    assert abs(sir(out, tgt, itf) - float(g["sir_out"])) <= SIR_TOL
+
+
+# ----------------------------------------------------------------------------- external mask
+@pytest.mark.parametrize("n", [512, 1024])
+@pytest.mark.parametrize("floor", [0.05, None])
+def test_fused_external_mask(avz, gpu_device, n, floor):
+    mix, tgt, itf = triple_f32("set2", (10000, 42000))
+    _, _, S_t = O.stft(tgt, nperseg=n, noverlap=n // 2)
+    _, _, S_i = O.stft(itf, nperseg=n, noverlap=n // 2)
+    rng = np.random.default_rng(3)
+    # a soft "neural" target probability: IRM-like plus noise, clipped to [0, 1]
+    M = np.abs(S_t) ** 2 / (np.abs(S_t) ** 2 + np.abs(S_i) ** 2 + 1e-10)
+    M = np.clip(M + 0.1 * rng.standard_normal(M.shape), 0, 1).astype(np.float32)
+    ref = O.external_mask_vec(mix, M, n_fft=n, hop=n // 2, sigma=1e-5, d=0.04, floor=floor)
+    plan = avz.MVDRPlan(n_fft=n, sigma=1e-5, mic_d=0.04, mask="external",
+                        postfilter="floor" if floor is not None else "none",
+                        pf_floor=floor or 0.0, normalize="none", max_batch=1,
+                        max_samples=len(tgt))
+    out, peak = plan.run(dev_t(mix, gpu_device)[None], ext_mask=dev_t(M, gpu_device)[None])
+    torch.cuda.synchronize()
+    got = out[0, :len(ref)].cpu().numpy()
+    scale = np.max(np.abs(ref))
+    assert np.max(np.abs(got - ref)) <= WAVE_TOL * scale
+    assert abs(float(peak[0]) - scale) <= 1e-4 * scale
+
+
+# ----------------------------------------------------------------------------- batching
+@pytest.mark.parametrize("n", [512, 1024])
+def test_batch_ragged_lengths_match_single(avz, gpu_device, n):
+    """Variable-length utterances in one launch: each equals the oracle on its own."""
+    mix, tgt, itf = triple_f32("test")
+    lens = [n, n + 1, 5000, 16001, 64000, 40960]
+    S = max(lens)
+    offs = [0, 3000, 7000, 11000, 20000, 30000]
+    B = len(lens)
+    m = np.zeros((B, 2, S), np.float32)
+    t = np.zeros((B, S), np.float32)
+    i = np.zeros((B, S), np.float32)
+    for b, (L, o) in enumerate(zip(lens, offs)):
+        m[b, :, :L] = mix[:, o:o + L]
+        t[b, :L] = tgt[o:o + L]
+        i[b, :L] = itf[o:o + L]
+    plan = avz.MVDRPlan(n_fft=n, sigma=1e-5, mic_d=0.01, mask="ibm", postfilter="ibm",
+                        normalize="peak", max_batch=B, max_samples=S)
+    out, peak = plan.run(dev_t(m, gpu_device), torch.tensor(lens, dtype=torch.int32,
+                                                            device=gpu_device), max_len=S,
+                         ref_tgt=dev_t(t, gpu_device), ref_int=dev_t(i, gpu_device))
+    torch.cuda.synchronize()
+    out = out.cpu().numpy()
+    for b, L in enumerate(lens):
+        ref = O.oracle_debug_vec(m[b, :, :L], t[b, :L], i[b, :L], n_fft=n, hop=n // 2, sigma=1e-5)
+        assert np.max(np.abs(out[b, :len(ref)] - ref)) <= WAVE_TOL, b
+
+
+def test_plan_rejects_bad_shapes(avz, gpu_device):
+    plan = avz.MVDRPlan(n_fft=1024, mask="ibm", postfilter="ibm", max_batch=2, max_samples=4096)
+    x = torch.zeros((1, 2, 8192), device=gpu_device)
+    with pytest.raises(avz.AvzError):
+        plan.run(x, ref_tgt=x[:, 0], ref_int=x[:, 1])        # longer than max_samples
+    with pytest.raises(avz.AvzError):
+        plan.run(x[:, :, :2048])                             # IBM without references
+    with pytest.raises(avz.AvzError):
+        avz.MVDRPlan(n_fft=768)
