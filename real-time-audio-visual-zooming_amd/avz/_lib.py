@@ -8,6 +8,12 @@ from __future__ import annotations
 import ctypes as ct
 import os
 
+# PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7). Loading torch
+# first makes libavz.so's NEEDED libamdhip64.so.7 resolve to that same runtime, so
+# torch's device pointers and stream handles are valid for our launches. Loading
+# libavz first would map a second HIP runtime (/opt/rocm) into the process.
+import torch  # noqa: F401,E402
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AVZ_LIB", os.path.join(_HERE, "libavz.so"))
 
@@ -56,11 +62,27 @@ class AvzError(RuntimeError):
     pass
 
 
+def hip_runtimes_mapped() -> list:
+    """Paths of every libamdhip64 mapped into this process."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as fh:
+            for line in fh:
+                if "libamdhip64" in line:
+                    paths.add(os.path.realpath(line.split()[-1]))
+    except OSError:
+        pass
+    return sorted(paths)
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libavz.so not found at {LIB_PATH}; run __graft_entry__.build() "
                           "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
     lib = ct.CDLL(LIB_PATH)
+    rts = hip_runtimes_mapped()
+    if len(rts) > 1:
+        raise ImportError(f"two HIP runtimes mapped into the process: {rts}")
     P = ct.c_void_p
     lib.avz_plan_create.argtypes = [ct.POINTER(P), ct.POINTER(AvzConfig)]
     lib.avz_plan_destroy.argtypes = [P]

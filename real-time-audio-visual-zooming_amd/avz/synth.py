@@ -1,0 +1,92 @@
+"""Deterministic synthetic 2-mic scenes (the bench/test input generator).
+
+LJ-Speech cannot be fetched offline, so sources are "speech-like" (SURVEY.md 8(d)):
+Gaussian noise -> AR(2) spectral tilt (poles 0.9, 0.5) x a 4 Hz syllabic envelope
+with 25 % of 250-ms blocks silenced; rng seed 1000 + utterance index.
+
+Mixing follows the reference's anechoic far-field model:
+* delays  — full_audio_generating_pipeline/world_building.py:47-51
+* frac delay by rfft phase shift — world_building.py:53-59
+* interference gain for SIR 0 dB on mic 1 — Final_pipeline/src/simulation.py:167-179
+* AWGN per channel at SNR 5 dB — simulation.py:47-56, world.py:25, 93-98
+* shared peak normalisation of mix and refs — simulation.py:197-202
+* refs = mic-1 target and mic-1 total interference (world.py:236-238).
+Geometry: D = 0.08 m (Final_pipeline/src/config.py:29), target 90 deg,
+interferer 1 at 40 deg (world.py:33), further interferers uniform in [0, 180].
+"""
+from __future__ import annotations
+
+import numpy as np
+from scipy.signal import lfilter
+
+FS = 16000
+C_SOUND = 343.0
+MIC_D = 0.08
+
+
+def speech_like(rng: np.random.Generator, n: int, fs: int = FS) -> np.ndarray:
+    x = rng.standard_normal(n)
+    # AR(2) with poles 0.9, 0.5: y[n] = 1.4 y[n-1] - 0.45 y[n-2] + x[n]
+    y = lfilter([1.0], [1.0, -1.4, 0.45], x)
+    t = np.arange(n) / fs
+    env = np.abs(np.sin(2 * np.pi * 4.0 * t + rng.uniform(0, np.pi)))
+    blk = int(0.25 * fs)
+    nb = -(-n // blk)
+    keep = rng.random(nb) >= 0.25
+    env *= np.repeat(keep, blk)[:n]
+    return y * env
+
+
+def far_field_delays(azimuth_deg: float, d: float = MIC_D, c: float = C_SOUND):
+    th = np.deg2rad(azimuth_deg)
+    return (d / 2) * np.cos(th - 0) / c, (d / 2) * np.cos(th - np.pi) / c
+
+
+def frac_delay(y: np.ndarray, delay_s: float, fs: int = FS) -> np.ndarray:
+    n = len(y)
+    Yf = np.fft.rfft(y)
+    f = np.fft.rfftfreq(n, 1.0 / fs)
+    return np.fft.irfft(Yf * np.exp(-1j * 2 * np.pi * f * delay_s), n=n)
+
+
+def add_awgn(rng: np.random.Generator, s: np.ndarray, snr_db: float) -> np.ndarray:
+    p = np.mean(s ** 2)
+    if p == 0:
+        return s
+    return s + rng.normal(0, np.sqrt(p / (10 ** (snr_db / 10))), s.shape)
+
+
+def make_scene(idx: int, n_samples: int = 64000, n_interferers: int = 1, d: float = MIC_D,
+               sir_db: float = 0.0, snr_db: float = 5.0, fs: int = FS):
+    """One utterance. Returns (mix [2, S], target_ref [S], interference_ref [S]) float32."""
+    rng = np.random.default_rng(1000 + idx)
+    angles = [40.0] + list(rng.uniform(0.0, 180.0, max(0, n_interferers - 1)))
+    tgt = speech_like(rng, n_samples, fs)
+    t1, t2 = far_field_delays(90.0, d)
+    tgt_m = [frac_delay(tgt, t1, fs), frac_delay(tgt, t2, fs)]
+    int_m = [np.zeros(n_samples), np.zeros(n_samples)]
+    for a in angles[:n_interferers]:
+        s = speech_like(rng, n_samples, fs)
+        d1, d2 = far_field_delays(a, d)
+        int_m[0] += frac_delay(s, d1, fs)
+        int_m[1] += frac_delay(s, d2, fs)
+    p_t, p_i = np.mean(tgt_m[0] ** 2), np.mean(int_m[0] ** 2)
+    if n_interferers > 0 and p_i > 0:
+        g = np.sqrt(p_t / (p_i * 10 ** (sir_db / 10)))
+        int_m = [g * int_m[0], g * int_m[1]]
+    mix = np.stack([add_awgn(rng, tgt_m[0] + int_m[0], snr_db),
+                    add_awgn(rng, tgt_m[1] + int_m[1], snr_db)])
+    peak = np.max(np.abs(mix)) + 1e-9
+    return ((mix / peak).astype(np.float32), (tgt_m[0] / peak).astype(np.float32),
+            (int_m[0] / peak).astype(np.float32))
+
+
+def make_batch(batch: int, start: int = 0, n_samples: int = 64000, n_interferers: int = 2,
+               **kw):
+    """[B, 2, S] mix, [B, S] target ref, [B, S] interference ref (float32)."""
+    mix = np.empty((batch, 2, n_samples), np.float32)
+    tgt = np.empty((batch, n_samples), np.float32)
+    itf = np.empty((batch, n_samples), np.float32)
+    for b in range(batch):
+        mix[b], tgt[b], itf[b] = make_scene(start + b, n_samples, n_interferers, **kw)
+    return mix, tgt, itf

@@ -91,13 +91,15 @@ def test_fused_ibm_excerpt_vs_reference(avz, gpu_device, name):
     # stage parity against the oracle's fp64 covariance / weights
     _, st = O.oracle_debug_vec(mix, tgt, itf, n_fft=n, hop=n // 2, sigma=s, return_stages=True)
     msum = st["mask"].sum(axis=1)
-    # IBM counts are exact except where |S_int| ~ |S_tgt| to fp32 rounding (the GPU STFT is
-    # fp32; scipy's is fp64 rounded to complex64): every flipped bin must hold a near tie.
+    # IBM counts are exact except where |S_int| ~ |S_tgt| to within fp32 FFT rounding (the
+    # GPU STFT is fp32; scipy's is fp64 rounded to complex64). FFT error scales with the
+    # frame's largest bin, so a flipped bin must hold a tie relative to that scale.
     diff = np.nonzero(cov[:, 4] != msum)[0]
     assert len(diff) <= max(1, len(msum) // 100)
+    frame_scale = np.maximum(np.abs(st["S_i"]).max(axis=0), np.abs(st["S_t"]).max(axis=0))
     for k in diff:
         a, b = np.abs(st["S_i"][k]), np.abs(st["S_t"][k])
-        rel = np.abs(a - b) / np.maximum(np.maximum(a, b), 1e-30)
+        rel = np.abs(a - b) / np.maximum(frame_scale, 1e-30)
         assert np.min(rel) < 1e-5, (k, np.min(rel))
     ok = cov[:, 4] == msum
     R = st["R"] * (msum + 1e-6)[:, None, None]
