@@ -11,6 +11,14 @@
 //              in : lane L, reg r  <->  x[64 r + L]
 //              out: lane (k1 = L&31, h = L>>5), reg k'  <->  X[k1 + 32 k' + 512 h]
 //
+//  Fft1024x2 : two independent 1024-point FFTs per wave (lane group g = L>>5),
+//              32 points per lane, NO cross-lane ops: N = 32 (n1, registers) x 32 (l).
+//              step 1: 32-pt DFT in registers; twiddle W1024^{l k1} from an LDS table
+//                      [k1][l] (conflict-free); LDS transpose (32 x 33 float2 per group);
+//              step 2: 32-pt DFT in registers.
+//              in : lane (l = L&31, g), reg r  <->  x_g[l + 32 r]
+//              out: lane (l, g), reg k  <->  X_g[l + 32 k]
+//
 //  Fft512x2  : two independent 512-point FFTs per wave (lane group g = L>>5).
 //              N = 16 (n1, registers) x 32 (j, lanes).
 //              step 1: 16-pt DFT in registers; twiddle W512^{j k1};
@@ -155,6 +163,22 @@ __device__ __forceinline__ void xhalf_dit(cf (&v)[16], float sgn) {
   });
 }
 
+// In-place forward 32-point DFT on registers (DIT: two 16-point DFTs + radix 2).
+__device__ __forceinline__ void dft32(cf (&v)[32]) {
+  cf e[16], o[16];
+  static_for<0, 16>([&](auto i) {
+    e[i] = v[2 * i];
+    o[i] = v[2 * i + 1];
+  });
+  dft16(e);
+  dft16(o);
+  static_for<0, 16>([&](auto k) {
+    const cf t = w32mul<k>(o[k]);
+    v[k] = c_add(e[k], t);
+    v[k + 16] = c_sub(e[k], t);
+  });
+}
+
 __device__ __forceinline__ cf unit_root(double frac) {
   // exp(-2 pi i frac), evaluated in fp64 then rounded
   double s, c;
@@ -165,6 +189,7 @@ __device__ __forceinline__ cf unit_root(double frac) {
 // -------------------------------------------------------------------- Fft1024
 struct Fft1024 {
   static constexpr int N = 1024;
+  static constexpr int PPL = 16;
   static constexpr int SCRATCH_F2 = 32 * 33;  // float2 elements of LDS scratch
   cf P[4], Q[4];  // W^{l j} (j<4), W^{l (4 i + 16 h)} (i<4)
   float sgn;
@@ -198,9 +223,38 @@ struct Fft1024 {
   }
 };
 
+// -------------------------------------------------------------------- Fft1024x2
+struct Fft1024x2 {
+  static constexpr int N = 1024;
+  static constexpr int PPL = 32;  // points per lane
+  int l;
+
+  __device__ __forceinline__ void init(int lane) { l = lane & 31; }
+
+  // Fill the block-shared twiddle table tw[k1 * 32 + l] = W1024^{l k1}.
+  __device__ static void fill_twiddles(cf* tw, int tid, int nthreads) {
+    for (int i = tid; i < 32 * 32; i += nthreads) {
+      const int k1 = i >> 5, ll = i & 31;
+      tw[i] = unit_root((double)(ll * k1) / N);
+    }
+  }
+
+  // v: x_g[l + 32 r] in; X_g[l + 32 k] out. scratch: this lane group's slot.
+  __device__ __forceinline__ void forward(cf (&v)[32], cf* scratch, const cf* tw) const {
+    dft32(v);
+    static_for<1, 32>([&](auto k) { v[k] = c_mul(v[k], tw[k * 32 + l]); });
+    static_for<0, 32>([&](auto k) { scratch[k * 33 + l] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 32>([&](auto r) { v[r] = scratch[l * 33 + r]; });
+    __builtin_amdgcn_wave_barrier();
+    dft32(v);
+  }
+};
+
 // -------------------------------------------------------------------- Fft512x2
 struct Fft512x2 {
   static constexpr int N = 512;
+  static constexpr int PPL = 16;
   static constexpr int SCRATCH_F2 = 16 * 34;  // per group
   cf P[4], Q[4];  // W512^{j i}, W512^{4 j i}
   float sgn;      // step-2 half: (lane >> 4) & 1
@@ -217,8 +271,10 @@ struct Fft512x2 {
     for (int i = 0; i < 4; ++i) Q[i] = unit_root((double)(4 * j * i) / N);
   }
 
+  __device__ static void fill_twiddles(cf*, int, int) {}
+
   // v: x_g[j + 32 r] in; X_g[k1 + 16 r + 256 h] out. scratch: this lane group's slot.
-  __device__ __forceinline__ void forward(cf (&v)[16], cf* scratch) const {
+  __device__ __forceinline__ void forward(cf (&v)[16], cf* scratch, const cf* = nullptr) const {
     dft16(v);  // reg k holds A[j][k]
     static_for<1, 16>([&](auto k) {
       const cf tw = ((k & 3) == 0) ? Q[k >> 2] : c_mul(P[k & 3], Q[k >> 2]);

@@ -51,21 +51,25 @@ template <int N>
 struct KCfg;
 template <>
 struct KCfg<1024> {
-  using Fft = Fft1024;
-  static constexpr int FPW = 1;              // FFTs per wave
+  using Fft = Fft1024x2;
+  static constexpr int PPL = Fft::PPL;       // complex points per lane
+  static constexpr int FPW = 2;              // FFTs per wave (lane groups of 32)
   static constexpr int GROUP_BYTES = 32 * 33 * 8;
-  static constexpr int WAVE_BYTES = GROUP_BYTES;
-  static constexpr int IN_STRIDE = 64;       // sample stride between registers
+  static constexpr int WAVE_BYTES = 2 * GROUP_BYTES;
+  static constexpr int IN_STRIDE = 32;       // sample stride between registers
   static constexpr int OUT_STRIDE = 32;      // bin/time stride between registers
+  static constexpr int TW_BYTES = 32 * 32 * 8;  // block-shared W1024^{l k1} table
 };
 template <>
 struct KCfg<512> {
   using Fft = Fft512x2;
+  static constexpr int PPL = Fft::PPL;
   static constexpr int FPW = 2;
   static constexpr int GROUP_BYTES = 16 * 34 * 8;
   static constexpr int WAVE_BYTES = 2 * GROUP_BYTES;
   static constexpr int IN_STRIDE = 32;
   static constexpr int OUT_STRIDE = 16;
+  static constexpr int TW_BYTES = 0;
 };
 
 template <int N, int NT = kThreads>
@@ -78,8 +82,12 @@ struct Geo {
   static constexpr int Q = NT / NB;         // frame groups in the per-bin phase
   static constexpr int NSLOT = NWAVE * C::FPW;
   static constexpr int SLOT_LDS = NWAVE * C::WAVE_BYTES;
-  // + double-buffered OLA carry + Nyquist-bin running sums [Q][5] fp64 + its 2 apply coefs
-  static constexpr int LDS_BYTES = SLOT_LDS + 2 * H * 4 + Q * 5 * 8 + 16;
+  // LDS map: [FFT slots][OLA carry 2 x H f32][twiddles][Nyquist sums Q x 5 f64][2 coefs]
+  static constexpr int CARRY_OFF = SLOT_LDS;
+  static constexpr int TW_OFF = CARRY_OFF + 2 * H * 4;
+  static constexpr int NYQ_OFF = TW_OFF + C::TW_BYTES;
+  static constexpr int LDS_BYTES = NYQ_OFF + Q * 5 * 8 + 16;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
   static_assert(NB * 5 * 8 * Q <= SLOT_LDS, "covariance reduction must fit the slot area");
 };
 
@@ -97,9 +105,9 @@ struct LaneMap {
   int out0;   // output index of register 0
   __device__ __forceinline__ void init(int lane) {
     if constexpr (N == 1024) {
-      in0 = lane;
-      grp = 0;
-      out0 = (lane & 31) + 512 * (lane >> 5);
+      in0 = lane & 31;
+      grp = lane >> 5;
+      out0 = lane & 31;
     } else {
       in0 = lane & 31;
       grp = lane >> 5;
@@ -222,11 +230,14 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
   constexpr int FPT1 = FB1 / Q;                                  // frames per thread, pass 1
   constexpr int FB2 = NSLOT;
   constexpr int FPT2 = FB2 / Q;
-  static_assert(MASK != MASK_IBM || FPT1 == 4, "IBM nibble layout assumes 4 frames/thread");
-  static_assert(FPT2 == 8, "pass-2 layout assumes 8 frames/thread");
+  constexpr int PPL = C::PPL;
+  static_assert(FPT1 % 4 == 0 && FPT2 % 4 == 0, "mask nibbles hold 4 frames");
+  static_assert(FPT2 % 2 == 0 && FPT2 <= 32, "pass-2 frame pairs");
 
   extern __shared__ __align__(16) unsigned char lds[];
-  float* carry = reinterpret_cast<float*>(lds + G::SLOT_LDS);  // [2][H]
+  float* carry = reinterpret_cast<float*>(lds + G::CARRY_OFF);  // [2][H]
+  cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
+  C::Fft::fill_twiddles(twid, threadIdx.x, NT);
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -279,7 +290,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
     r_i = make_rsrc(A.ref_int + (long long)b * A.ref_stride, L);
   }
 
-  cf v[16];
+  cf v[PPL];
   auto issue_loads = [&](int step) {
     bool ref = false;
     int frame;
@@ -296,20 +307,21 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
     const rsrc_t re = ref ? r_t : r_m0;
     const rsrc_t im = ref ? r_i : r_m1;
     const int s0 = frame * H - N / 2 + lm.in0;
-    static_for<0, 16>([&](auto r) {
+    static_for<0, PPL>([&](auto r) {
       v[r].x = bload(re, s0 + C::IN_STRIDE * r);
       v[r].y = bload(im, s0 + C::IN_STRIDE * r);
     });
   };
   auto window_and_fft = [&]() {
-    static_for<0, 16>([&](auto r) {
-      constexpr float cr = W32::c[2 * r], sr = -W32::s[2 * r];  // cos, sin of 2 pi r / 16
+    static_for<0, PPL>([&](auto r) {
+      constexpr int j = (C::IN_STRIDE * 32 / N) * r;  // 2 pi (IN_STRIDE r)/N = 2 pi j/32
+      constexpr float cr = W32::c[j % 32], sr = -W32::s[j % 32];
       const float w = fmaf(was, sr, fmaf(-wac, cr, wa0));
       v[r] = c_scale(v[r], w);
     });
-    fft.forward(v, my_spec);
+    fft.forward(v, my_spec, twid);
     // natural-order spectrum into this lane group's slot
-    static_for<0, 16>([&](auto k) { my_spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
+    static_for<0, PPL>([&](auto k) { my_spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
   };
 
   // ---------------- per-bin thread role
@@ -321,7 +333,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
   const bool nyq = (kb == 0);
   const int kp = (N - kb) & (N - 1);
   uint8_t* mb = A.maskbits + (long long)b * A.mb_stride;
-  double* nyq_acc = reinterpret_cast<double*>(lds + G::SLOT_LDS + 2 * H * 4);  // [Q][5]
+  double* nyq_acc = reinterpret_cast<double*>(lds + G::NYQ_OFF);  // [Q][5]
   cf* nyq_ab = reinterpret_cast<cf*>(nyq_acc + Q * 5);                        // alpha_n, beta_n
   cf alpha{0, 0}, beta{0, 0};
 
@@ -354,6 +366,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
     for (int c = 0; c < 5; ++c) nyq_acc[q * 5 + c] = 0.0;
   }
   issue_loads(0);
+  lds_barrier();  // twiddle table + Nyquist sums initialised
   {
     Acc64 acc;
     acc.zero();
@@ -403,11 +416,15 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
         nyq_acc[q * 5 + 3] += (double)an.c01i;
         nyq_acc[q * 5 + 4] += (double)an.cm;
         if constexpr (MASK == MASK_IBM) {
-          if (tq < T) mb[(long long)(tq >> 2) * F + N / 2] = (uint8_t)nibn;
+          for (int j = 0; j < FPT1 / 4; ++j)
+            if (tq + 4 * j < T)
+              mb[(long long)((tq >> 2) + j) * F + N / 2] = (uint8_t)(nibn >> (4 * j));
         }
       }
       if constexpr (MASK == MASK_IBM) {
-        if (tq < T) mb[(long long)(tq >> 2) * F + kb] = (uint8_t)nib;
+#pragma unroll
+        for (int j = 0; j < FPT1 / 4; ++j)
+          if (tq + 4 * j < T) mb[(long long)((tq >> 2) + j) * F + kb] = (uint8_t)(nib >> (4 * j));
       }
       lds_barrier();
     }
@@ -446,10 +463,11 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
   }
 
   // ============ pass 2: apply + post-filter + iSTFT overlap-add ============
-  // OLA role: 4 consecutive samples m of segments {sgrp, sgrp + NSG}
+  // OLA role: 4 consecutive samples m of segments {sgrp + i NSG}
   constexpr int M4 = N / 8;  // float4 groups per half frame
   constexpr int NSG = NT / M4;
-  static_assert(2 * NSG == FB2, "OLA mapping");
+  constexpr int SPT = FB2 / NSG;  // segments per thread
+  static_assert(SPT * NSG == FB2, "OLA mapping");
   const int m0 = 4 * (tid % M4);
   const int sgrp = tid / M4;
   float peak = 0.0f;
@@ -480,10 +498,11 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
       };
       auto load_bits = [&](int kk) -> uint32_t {  // bit i: frame tq + i is noise (IBM)
         uint32_t bb = 0;
-        if (A.postfilter == PF_IBM_TARGET && tq < T) {
+        if (A.postfilter == PF_IBM_TARGET) {
           const uint8_t* row = mb + (long long)(tq >> 2) * F;
-          bb = row[kk];
-          if (tq + 4 < T) bb |= (uint32_t)row[F + kk] << 4;
+#pragma unroll
+          for (int j = 0; j < FPT2 / 4; ++j)
+            if (tq + 4 * j < T) bb |= (uint32_t)row[j * F + kk] << (4 * j);
         }
         return bb;
       };
@@ -525,10 +544,10 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
     if (ifft_wave) {
       const int p = wave * C::FPW + lm.grp;
       cf* Zi = slot_ptr<N>(lds, 2 * p);
-      static_for<0, 16>([&](auto r) { v[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
-      fft.forward(v, Zi);
+      static_for<0, PPL>([&](auto r) { v[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
+      fft.forward(v, Zi, twid);
       float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
-      static_for<0, 16>([&](auto k) {
+      static_for<0, PPL>([&](auto k) {
         constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
         const float w = fmaf(wss, sk, fmaf(-wsc, ck, ws0));
         const int n = lm.out0 + C::OUT_STRIDE * k;
@@ -549,7 +568,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
         return reinterpret_cast<const float*>(slot_ptr<N>(lds, 2 * (f >> 1) + 1)) + (f & 1) * N;
       };
 #pragma unroll
-      for (int si = 0; si < 2; ++si) {
+      for (int si = 0; si < SPT; ++si) {
         const int s = sgrp + si * NSG;
         const int j = f0 - 1 + s;
         if (j >= 0 && j <= T - 2) {
@@ -607,18 +626,23 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
 // Standalone STFT (stage API / parity): Y[b][c][k][t] = scipy.signal.stft(x[b][c])
 // One block per (utterance, NSLOT-frame batch); each lane group transforms one
 // frame of the packed channel pair, then threads split the pair per bin.
+constexpr int kStftThreads = 512;
+
 template <int N>
-__global__ void __launch_bounds__(kThreads, 1) avz_stft_kernel(StftArgs A) {
+__global__ void __launch_bounds__(kStftThreads, 1) avz_stft_kernel(StftArgs A) {
   using C = KCfg<N>;
-  using G = Geo<N>;
-  constexpr int H = G::H, F = G::F, NSLOT = G::NSLOT;
+  using G = Geo<N, kStftThreads>;
+  constexpr int H = G::H, F = G::F, NSLOT = G::NSLOT, PPL = C::PPL;
   extern __shared__ __align__(16) unsigned char lds[];
+  cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
+  C::Fft::fill_twiddles(twid, threadIdx.x, kStftThreads);
   const int b = blockIdx.x;
   const int f0 = blockIdx.y * NSLOT;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int L = A.len[b];
   const int T = (L + H - 1) / H + 1;
-  if (f0 >= T) return;
+  if (f0 >= T || L < N) return;
+  __syncthreads();
 
   typename C::Fft fft;
   fft.init(lane);
@@ -638,25 +662,25 @@ __global__ void __launch_bounds__(kThreads, 1) avz_stft_kernel(StftArgs A) {
     wac = (float)(0.5 * sc * c);
     was = (float)(0.5 * sc * s);
   }
-  cf v[16];
+  cf v[PPL];
   const int s0 = (f0 + my_slot) * H - N / 2 + lm.in0;
-  static_for<0, 16>([&](auto r) {
-    constexpr float cr = W32::c[2 * r], sr = -W32::s[2 * r];
+  static_for<0, PPL>([&](auto r) {
+    constexpr int j = (C::IN_STRIDE * 32 / N) * r;
+    constexpr float cr = W32::c[j % 32], sr = -W32::s[j % 32];
     const float w = fmaf(was, sr, fmaf(-wac, cr, wa0));
     v[r] = {bload(re, s0 + C::IN_STRIDE * r) * w, bload(im, s0 + C::IN_STRIDE * r) * w};
   });
-  fft.forward(v, spec);
-  static_for<0, 16>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
+  fft.forward(v, spec, twid);
+  static_for<0, PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
   __syncthreads();
   float2* Y = reinterpret_cast<float2*>(A.Y);
-  for (int idx = tid; idx < F * NSLOT; idx += kThreads) {
+  for (int idx = tid; idx < F * NSLOT; idx += kStftThreads) {
     const int k = idx / NSLOT, f = idx % NSLOT;
     const int t = f0 + f;
     if (t >= T) continue;
     const cf* Z = slot_ptr<N>(lds, f);
     cf a, c;
-    if (k == 0 || k == N / 2) split_self(Z[k], a, c);
-    else split_pair(Z[k], Z[N - k], a, c);
+    split_pair(Z[k], Z[(N - k) & (N - 1)], a, c);
     const long long o = (long long)b * A.y_stride_b + (long long)k * A.y_stride_f + t;
     Y[o] = make_float2(a.x, a.y);
     if (A.channels > 1) Y[o + A.y_stride_c] = make_float2(c.x, c.y);
@@ -714,7 +738,7 @@ extern "C" int avz_launch_fused(int n_fft, int mask_mode, const FusedArgs* a, vo
 template <int N>
 static int launch_stft_t(const StftArgs* a, hipStream_t st) {
   auto kern = avz_stft_kernel<N>;
-  const int lds = Geo<N>::SLOT_LDS;
+  const int lds = Geo<N, kStftThreads>::LDS_BYTES;
   static bool attr_done = false;
   if (!attr_done) {
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
@@ -722,8 +746,9 @@ static int launch_stft_t(const StftArgs* a, hipStream_t st) {
       return -3;
     attr_done = true;
   }
-  dim3 grid(a->batch, (a->max_frames + Geo<N>::NSLOT - 1) / Geo<N>::NSLOT);
-  hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, st, *a);
+  constexpr int NS = Geo<N, kStftThreads>::NSLOT;
+  dim3 grid(a->batch, (a->max_frames + NS - 1) / NS);
+  hipLaunchKernelGGL(kern, grid, dim3(kStftThreads), lds, st, *a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
