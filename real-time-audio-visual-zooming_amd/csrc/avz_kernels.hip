@@ -40,6 +40,25 @@ __device__ __forceinline__ float bload(rsrc_t r, int elem) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
 
+// Diagnostic build only (-DAVZ_STAMPS): wave 0 accumulates s_memrealtime (100 MHz)
+// deltas per phase into g_stamps[block][phase]. Phases: 0 pass-1 FFT, 1 pass-1 bins,
+// 2 solve, 3 pass-2 FFT, 4 pass-2 bins, 5 inverse FFT, 6 overlap-add, 7 peak/normalise.
+#ifdef AVZ_STAMPS
+__device__ unsigned long long* g_stamps;
+#define AVZ_STAMP_INIT() unsigned long long stamp_prev = __builtin_amdgcn_s_memrealtime()
+#define AVZ_STAMP(i)                                                        \
+  do {                                                                      \
+    if (threadIdx.x == 0 && g_stamps) {                                     \
+      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();     \
+      g_stamps[blockIdx.x * 8 + (i)] += now_ - stamp_prev;                  \
+      stamp_prev = now_;                                                    \
+    }                                                                       \
+  } while (0)
+#else
+#define AVZ_STAMP_INIT() (void)0
+#define AVZ_STAMP(i) (void)0
+#endif
+
 // LDS-only barrier: leaves global loads (the next frame's prefetch) in flight.
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -326,15 +345,17 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
 
   // ---------------- per-bin thread role
   // Thread (kb, q) owns bin kb for the frames of row q. Bin 0 is self-partnered
-  // (kp = 0) and needs no special case; the Nyquist bin N/2 is extra work of the
-  // kb == 0 threads, with its running state kept in LDS.
+  // (kp = 0) and needs no special case. The Nyquist bin N/2 is spread over lanes of
+  // the last wave (one frame, or frame pair, per lane) so no wave carries it alone;
+  // its running sums live in LDS.
   const int kb = tid % NB;
   const int q = tid / NB;
   const bool nyq = (kb == 0);
   const int kp = (N - kb) & (N - 1);
+  const bool nyq_wave = (wave == NWAVE - 1);
   uint8_t* mb = A.maskbits + (long long)b * A.mb_stride;
-  double* nyq_acc = reinterpret_cast<double*>(lds + G::NYQ_OFF);  // [Q][5]
-  cf* nyq_ab = reinterpret_cast<cf*>(nyq_acc + Q * 5);                        // alpha_n, beta_n
+  double* nyq_acc = reinterpret_cast<double*>(lds + G::NYQ_OFF);  // [5]
+  cf* nyq_ab = reinterpret_cast<cf*>(nyq_acc + Q * 5);            // alpha_n, beta_n
   cf alpha{0, 0}, beta{0, 0};
 
   auto bin_weight = [&](cf x0, cf x1, const cf* Zr, int k, int kk, int t, bool& noise,
@@ -361,12 +382,10 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
   };
 
   // ======================= pass 1: masks + covariance =======================
-  if (nyq) {
-#pragma unroll
-    for (int c = 0; c < 5; ++c) nyq_acc[q * 5 + c] = 0.0;
-  }
+  if (tid < 5) nyq_acc[tid] = 0.0;
   issue_loads(0);
   lds_barrier();  // twiddle table + Nyquist sums initialised
+  AVZ_STAMP_INIT();
   {
     Acc64 acc;
     acc.zero();
@@ -374,51 +393,61 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
       window_and_fft();
       issue_loads(step + 1);  // step NB1 is pass 2's first batch
       lds_barrier();
+      AVZ_STAMP(0);
       const int f0 = step * FB1;
       const int tq = f0 + q * FPT1;
       Acc32 a32;
       a32.zero();
       unsigned nib = 0;
-#pragma unroll 1
+      const int nvalid = T - tq;  // frames of this row that exist (may be <= 0)
+#pragma unroll 4
       for (int i = 0; i < FPT1; ++i) {
-        const int f = q * FPT1 + i;
-        if (tq + i >= T) break;
-        const cf* Zm = slot_ptr<N>(lds, f);
-        cf x0, x1;
-        split_pair(Zm[kb], Zm[kp], x0, x1);
-        bool noise = false;
-        float wgt;
-        const float m = bin_weight(x0, x1, slot_ptr<N>(lds, FB1 + f), kb, kp, tq + i, noise, wgt);
-        nib |= (noise ? 1u : 0u) << i;
-        a32.add(x0, x1, wgt, m);
+        if (i < nvalid) {
+          const int f = q * FPT1 + i;
+          const cf* Zm = slot_ptr<N>(lds, f);
+          cf x0, x1;
+          split_pair(Zm[kb], Zm[kp], x0, x1);
+          bool noise = false;
+          float wgt;
+          const float m =
+              bin_weight(x0, x1, slot_ptr<N>(lds, FB1 + f), kb, kp, tq + i, noise, wgt);
+          nib |= (noise ? 1u : 0u) << i;
+          a32.add(x0, x1, wgt, m);
+        }
       }
       acc.add(a32);
-      if (nyq) {  // Nyquist bin: self-partnered, running sums in LDS
+      if (nyq_wave) {  // Nyquist bin: frame `lane` of the batch on lane `lane`
         Acc32 an;
         an.zero();
-        unsigned nibn = 0;
-        for (int i = 0; i < FPT1; ++i) {
-          const int f = q * FPT1 + i;
-          if (tq + i >= T) break;
+        bool noise = false;
+        if (lane < FB1 && f0 + lane < T) {
+          const cf* Zm = slot_ptr<N>(lds, lane);
           cf y0, y1;
-          const cf* Zm = slot_ptr<N>(lds, f);
           split_pair(Zm[N / 2], Zm[N / 2], y0, y1);
-          bool noise = false;
           float wn;
-          const float mn = bin_weight(y0, y1, slot_ptr<N>(lds, FB1 + f), N / 2, N / 2, tq + i,
-                                      noise, wn);
-          nibn |= (noise ? 1u : 0u) << i;
+          const float mn = bin_weight(y0, y1, slot_ptr<N>(lds, FB1 + lane), N / 2, N / 2,
+                                      f0 + lane, noise, wn);
           an.add(y0, y1, wn, mn);
         }
-        nyq_acc[q * 5 + 0] += (double)an.c00;
-        nyq_acc[q * 5 + 1] += (double)an.c11;
-        nyq_acc[q * 5 + 2] += (double)an.c01r;
-        nyq_acc[q * 5 + 3] += (double)an.c01i;
-        nyq_acc[q * 5 + 4] += (double)an.cm;
-        if constexpr (MASK == MASK_IBM) {
-          for (int j = 0; j < FPT1 / 4; ++j)
-            if (tq + 4 * j < T)
-              mb[(long long)((tq >> 2) + j) * F + N / 2] = (uint8_t)(nibn >> (4 * j));
+        for (int o = 1; o < FB1; o <<= 1) {
+          an.c00 += __shfl_xor(an.c00, o, 64);
+          an.c11 += __shfl_xor(an.c11, o, 64);
+          an.c01r += __shfl_xor(an.c01r, o, 64);
+          an.c01i += __shfl_xor(an.c01i, o, 64);
+          an.cm += __shfl_xor(an.cm, o, 64);
+        }
+        const unsigned long long bal = __ballot(noise);
+        if (lane == 0) {
+          nyq_acc[0] += (double)an.c00;
+          nyq_acc[1] += (double)an.c11;
+          nyq_acc[2] += (double)an.c01r;
+          nyq_acc[3] += (double)an.c01i;
+          nyq_acc[4] += (double)an.cm;
+          if constexpr (MASK == MASK_IBM) {
+            for (int j = 0; j < FB1 / 4; ++j)
+              if (f0 + 4 * j < T)
+                mb[(long long)((f0 >> 2) + j) * F + N / 2] = (uint8_t)((bal >> (4 * j)) & 15u);
+          }
         }
       }
       if constexpr (MASK == MASK_IBM) {
@@ -427,6 +456,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
           if (tq + 4 * j < T) mb[(long long)((tq >> 2) + j) * F + kb] = (uint8_t)(nib >> (4 * j));
       }
       lds_barrier();
+      AVZ_STAMP(1);
     }
 
     // ============ solve: reduce the Q partial rows, fp64 MVDR ============
@@ -447,11 +477,9 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
       for (int c = 0; c < 5; ++c) A.cov_out[((long long)b * F + kb) * 5 + c] = R[c];
     }
     if (tid == 0) {
-      double Rn[5] = {0, 0, 0, 0, 0};
-      for (int qq = 0; qq < Q; ++qq) {
+      double Rn[5];
 #pragma unroll
-        for (int c = 0; c < 5; ++c) Rn[c] += nyq_acc[qq * 5 + c];
-      }
+      for (int c = 0; c < 5; ++c) Rn[c] = nyq_acc[c];
       float* wdbgn = A.w_out ? A.w_out + ((long long)b * F + N / 2) * 4 : nullptr;
       mvdr_solve(Rn, N / 2, N, A, nyq_ab[0], nyq_ab[1], wdbgn);
       if (A.cov_out) {
@@ -460,6 +488,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
       }
     }
     lds_barrier();
+    AVZ_STAMP(2);
   }
 
   // ============ pass 2: apply + post-filter + iSTFT overlap-add ============
@@ -479,6 +508,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
     window_and_fft();
     if (!ifft_wave && more) issue_loads(step + 1);  // idle during the inverse FFT: prefetch now
     lds_barrier();
+    AVZ_STAMP(3);
 
     const int f0 = st2 * FB2;
     const int tq = f0 + q * FPT2;
@@ -507,38 +537,40 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
         return bb;
       };
       const uint32_t bits = load_bits(kb);
-#pragma unroll 1
+#pragma unroll 2
       for (int pi = 0; pi < FPT2 / 2; ++pi) {
         const int fa = q * FPT2 + 2 * pi;
         const int ta = tq + 2 * pi;
-        if (ta >= T) break;
-        cf* Za = slot_ptr<N>(lds, fa);
-        const cf* Zb = slot_ptr<N>(lds, fa + 1);
-        const float ga = gain(2 * pi, ta, bits, kb), gb = gain(2 * pi + 1, ta + 1, bits, kb);
-        const cf za = Za[kb], zap = Za[kp], zb = Zb[kb], zbp = Zb[kp];
-        const cf sa = apply_bin(alpha, beta, za, zap, ga);
-        const cf sb = apply_bin(alpha, beta, zb, zbp, gb);
-        Za[kp] = {sa.x + sb.y, sb.x - sa.y};  // conj(Sa) + i conj(Sb) at N - k
-        // Sa + i Sb at k; at DC irfft keeps only the real parts (written last: kp == kb)
-        Za[kb] = nyq ? cf{sa.x, sb.x} : cf{sa.x - sb.y, sa.y + sb.x};
-      }
-      if (nyq) {  // Nyquist bin
-        const uint32_t bitsn = load_bits(N / 2);
-        const cf an = nyq_ab[0], bn = nyq_ab[1];
-        for (int pi = 0; pi < FPT2 / 2; ++pi) {
-          const int fa = q * FPT2 + 2 * pi;
-          const int ta = tq + 2 * pi;
-          if (ta >= T) break;
+        if (ta < T) {
           cf* Za = slot_ptr<N>(lds, fa);
           const cf* Zb = slot_ptr<N>(lds, fa + 1);
-          const float ga = gain(2 * pi, ta, bitsn, N / 2);
-          const float gb = gain(2 * pi + 1, ta + 1, bitsn, N / 2);
+          const float ga = gain(2 * pi, ta, bits, kb), gb = gain(2 * pi + 1, ta + 1, bits, kb);
+          const cf za = Za[kb], zap = Za[kp], zb = Zb[kb], zbp = Zb[kp];
+          const cf sa = apply_bin(alpha, beta, za, zap, ga);
+          const cf sb = apply_bin(alpha, beta, zb, zbp, gb);
+          Za[kp] = {sa.x + sb.y, sb.x - sa.y};  // conj(Sa) + i conj(Sb) at N - k
+          // Sa + i Sb at k; at DC irfft keeps only the real parts (written last: kp == kb)
+          Za[kb] = nyq ? cf{sa.x, sb.x} : cf{sa.x - sb.y, sa.y + sb.x};
+        }
+      }
+      if (nyq_wave && lane < FB2 / 2) {  // Nyquist bin: frame pair `lane` on lane `lane`
+        const int fa = 2 * lane;
+        const int ta = f0 + fa;
+        if (ta < T) {
+          uint32_t bn = 0;
+          if (A.postfilter == PF_IBM_TARGET)
+            bn = (uint32_t)mb[(long long)(ta >> 2) * F + N / 2] >> (ta & 3);
+          const cf an = nyq_ab[0], bnn = nyq_ab[1];
+          cf* Za = slot_ptr<N>(lds, fa);
+          const cf* Zb = slot_ptr<N>(lds, fa + 1);
+          const float ga = gain(0, ta, bn, N / 2), gb = gain(1, ta + 1, bn, N / 2);
           const cf za = Za[N / 2], zb = Zb[N / 2];
-          Za[N / 2] = {apply_bin(an, bn, za, za, ga).x, apply_bin(an, bn, zb, zb, gb).x};
+          Za[N / 2] = {apply_bin(an, bnn, za, za, ga).x, apply_bin(an, bnn, zb, zb, gb).x};
         }
       }
     }
     lds_barrier();
+    AVZ_STAMP(4);
 
     // ---- inverse FFT of packed pairs -> windowed frame contributions (waves < NPAIR/FPW)
     if (ifft_wave) {
@@ -557,6 +589,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
       if (more) issue_loads(step + 1);
     }
     lds_barrier();
+    AVZ_STAMP(5);
 
     // ---- overlap-add: segment j = frame j (2nd half) + frame j+1 (1st half)
     {
@@ -598,6 +631,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
       }
     }
     lds_barrier();
+    AVZ_STAMP(6);
   }
 
   // ---------------- block max |out|, optional in-place normalisation
@@ -620,6 +654,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
       o4[i] = x;
     }
   }
+  AVZ_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------
@@ -695,6 +730,12 @@ using namespace avz;
 #define AVZ_FUSED_THREADS 512
 #endif
 constexpr int kFusedThreads = AVZ_FUSED_THREADS;
+
+#ifdef AVZ_STAMPS
+extern "C" int avz_debug_set_stamps(void* dev_ptr) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -3;
+}
+#endif
 
 extern "C" int avz_fused_lds_bytes(int n_fft) {
   return n_fft == 1024 ? Geo<1024, kFusedThreads>::LDS_BYTES

@@ -1,0 +1,62 @@
+"""Per-phase time breakdown of the fused kernel (diagnostic build libavz_stamps.so).
+
+Wave 0 of every block accumulates s_memrealtime (100 MHz) deltas between the
+kernel's barriers; this prints the mean per block in microseconds. The stamped build
+has extra scalar work in wave 0, so read the SHARES, not the absolute total.
+
+  AVZ_LIB=.../libavz_stamps.so python tools/phase_profile.py [--batch 256] [--mask ibm]
+"""
+import argparse
+import ctypes as ct
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "real-time-audio-visual-zooming_amd")]
+os.environ.setdefault("AVZ_LIB", os.path.join(ROOT, "real-time-audio-visual-zooming_amd", "avz",
+                                              "libavz_stamps.so"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import avz  # noqa: E402
+from avz import synth  # noqa: E402
+
+PHASES = ["p1 FFT", "p1 bins", "solve", "p2 FFT", "p2 bins", "iFFT", "OLA", "peak/norm"]
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=256)
+ap.add_argument("--n-fft", type=int, default=1024)
+ap.add_argument("--mask", default="ibm")
+ap.add_argument("--normalize", default="peak")
+ap.add_argument("--seconds", type=float, default=4.0)
+a = ap.parse_args()
+S = int(a.seconds * 16000)
+dev = torch.device("cuda:0")
+mix, tgt, itf = synth.make_batch(a.batch, n_samples=S, n_interferers=2)
+plan = avz.MVDRPlan(n_fft=a.n_fft, sigma=1.0, mic_d=0.01, mask=a.mask,
+                    postfilter="ibm" if a.mask == "ibm" else "none", normalize=a.normalize,
+                    max_batch=a.batch, max_samples=S)
+d = [torch.from_numpy(x).to(dev) for x in (mix, tgt, itf)]
+kw = dict(ref_tgt=d[1], ref_int=d[2]) if a.mask == "ibm" else {}
+st = torch.zeros((a.batch, 8), dtype=torch.int64, device=dev)
+lib = avz._lib.lib
+lib.avz_debug_set_stamps.argtypes = [ct.c_void_p]
+for _ in range(3):
+    plan.run(d[0], **kw)
+torch.cuda.synchronize()
+st.zero_()
+assert lib.avz_debug_set_stamps(ct.c_void_p(st.data_ptr())) == 0
+reps = 5
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(reps):
+    plan.run(d[0], **kw)
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / reps
+us = st.double().cpu().numpy() / reps / 100.0  # 100 MHz ticks -> us
+tot = us.sum(axis=1)
+print(f"kernel {ms*1e3:.1f} us/launch (stamped build), B={a.batch}, N={a.n_fft}, mask={a.mask}")
+print(f"per-block stamped total: mean {tot.mean():.1f} us, min {tot.min():.1f}, max {tot.max():.1f}")
+for i, n in enumerate(PHASES):
+    print(f"  {n:10s} {us[:, i].mean():8.1f} us  {100*us[:, i].mean()/tot.mean():5.1f} %")
