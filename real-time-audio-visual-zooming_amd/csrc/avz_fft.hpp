@@ -240,14 +240,38 @@ struct Fft1024x2 {
   }
 
   // v: x_g[l + 32 r] in; X_g[l + 32 k] out. scratch: this lane group's slot.
-  __device__ __forceinline__ void forward(cf (&v)[32], cf* scratch, const cf* tw) const {
+  // Twiddles are read from the LDS table in groups of 8 issued before their
+  // multiplies, so the read latency overlaps (one-at-a-time reads serialised it).
+  __device__ __forceinline__ void stage1(cf (&v)[32], const cf* tw) const {
+    cf t[8];
+    static_for<0, 8>([&](auto j) { t[j] = tw[(1 + j) * 32 + l]; });
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads issued ahead of the DFT
     dft32(v);
-    static_for<1, 32>([&](auto k) { v[k] = c_mul(v[k], tw[k * 32 + l]); });
+    static_for<0, 4>([&](auto g) {
+      static_for<0, 8>([&](auto j) {
+        constexpr int k = 8 * g + j + 1;
+        if constexpr (k < 32) v[k] = c_mul(v[k], t[j]);
+      });
+      if constexpr (g < 3) {
+        static_for<0, 8>([&](auto j) {
+          constexpr int k = 8 * (g + 1) + j + 1;
+          if constexpr (k < 32) t[j] = tw[k * 32 + l];
+        });
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+  }
+  __device__ __forceinline__ void transpose(cf (&v)[32], cf* scratch) const {
     static_for<0, 32>([&](auto k) { scratch[k * 33 + l] = v[k]; });
     __builtin_amdgcn_wave_barrier();
     static_for<0, 32>([&](auto r) { v[r] = scratch[l * 33 + r]; });
     __builtin_amdgcn_wave_barrier();
-    dft32(v);
+  }
+  __device__ __forceinline__ void stage2(cf (&v)[32]) const { dft32(v); }
+  __device__ __forceinline__ void forward(cf (&v)[32], cf* scratch, const cf* tw) const {
+    stage1(v, tw);
+    transpose(v, scratch);
+    stage2(v);
   }
 };
 

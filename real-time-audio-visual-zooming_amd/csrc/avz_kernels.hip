@@ -41,20 +41,24 @@ __device__ __forceinline__ float bload(rsrc_t r, int elem) {
 }
 
 // Diagnostic build only (-DAVZ_STAMPS): wave 0 accumulates s_memrealtime (100 MHz)
-// deltas per phase into g_stamps[block][phase]. Phases: 0 pass-1 FFT, 1 pass-1 bins,
-// 2 solve, 3 pass-2 FFT, 4 pass-2 bins, 5 inverse FFT, 6 overlap-add, 7 peak/normalise.
+// deltas per phase into g_stamps[block][16]. Phases: 0 pass-1 FFT (rest), 1 pass-1 bins,
+// 2 solve, 3 pass-2 FFT (rest), 4 pass-2 bins, 5 inverse FFT, 6 overlap-add,
+// 7 peak/normalise, 8 wait for prefetched samples, 9 FFT stage 1, 10 transpose,
+// 11 FFT stage 2 + spectrum store (8-11 summed over both passes, N = 1024 only).
 #ifdef AVZ_STAMPS
 __device__ unsigned long long* g_stamps;
-#define AVZ_STAMP_INIT() unsigned long long stamp_prev = __builtin_amdgcn_s_memrealtime()
+#define AVZ_STAMP_DECL() unsigned long long stamp_prev = 0
+#define AVZ_STAMP_INIT() stamp_prev = __builtin_amdgcn_s_memrealtime()
 #define AVZ_STAMP(i)                                                        \
   do {                                                                      \
     if (threadIdx.x == 0 && g_stamps) {                                     \
       const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();     \
-      g_stamps[blockIdx.x * 8 + (i)] += now_ - stamp_prev;                  \
+      g_stamps[blockIdx.x * 16 + (i)] += now_ - stamp_prev;                 \
       stamp_prev = now_;                                                    \
     }                                                                       \
   } while (0)
 #else
+#define AVZ_STAMP_DECL() (void)0
 #define AVZ_STAMP_INIT() (void)0
 #define AVZ_STAMP(i) (void)0
 #endif
@@ -310,6 +314,7 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
   }
 
   cf v[PPL];
+  AVZ_STAMP_DECL();
   auto issue_loads = [&](int step) {
     bool ref = false;
     int frame;
@@ -332,15 +337,34 @@ __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {
     });
   };
   auto window_and_fft = [&]() {
+#ifdef AVZ_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    AVZ_STAMP(8);
+#endif
     static_for<0, PPL>([&](auto r) {
       constexpr int j = (C::IN_STRIDE * 32 / N) * r;  // 2 pi (IN_STRIDE r)/N = 2 pi j/32
       constexpr float cr = W32::c[j % 32], sr = -W32::s[j % 32];
       const float w = fmaf(was, sr, fmaf(-wac, cr, wa0));
       v[r] = c_scale(v[r], w);
     });
+#if defined(AVZ_STAMPS)
+    if constexpr (N == 1024) {
+      fft.stage1(v, twid);
+      AVZ_STAMP(9);
+      fft.transpose(v, my_spec);
+      AVZ_STAMP(10);
+      fft.stage2(v);
+    } else {
+      fft.forward(v, my_spec, twid);
+    }
+#else
     fft.forward(v, my_spec, twid);
+#endif
     // natural-order spectrum into this lane group's slot
     static_for<0, PPL>([&](auto k) { my_spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
+#ifdef AVZ_STAMPS
+    AVZ_STAMP(11);
+#endif
   };
 
   // ---------------- per-bin thread role

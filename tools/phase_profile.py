@@ -21,7 +21,7 @@ import torch  # noqa: E402
 import avz  # noqa: E402
 from avz import synth  # noqa: E402
 
-PHASES = ["p1 FFT", "p1 bins", "solve", "p2 FFT", "p2 bins", "iFFT", "OLA", "peak/norm"]
+PHASES = ["p1 FFT rest", "p1 bins", "solve", "p2 FFT rest", "p2 bins", "iFFT", "OLA", "peak/norm", "load wait", "fft stage1", "fft transp", "fft stage2"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=256)
@@ -38,7 +38,7 @@ plan = avz.MVDRPlan(n_fft=a.n_fft, sigma=1.0, mic_d=0.01, mask=a.mask,
                     max_batch=a.batch, max_samples=S)
 d = [torch.from_numpy(x).to(dev) for x in (mix, tgt, itf)]
 kw = dict(ref_tgt=d[1], ref_int=d[2]) if a.mask == "ibm" else {}
-st = torch.zeros((a.batch, 8), dtype=torch.int64, device=dev)
+st = torch.zeros((a.batch, 16), dtype=torch.int64, device=dev)
 lib = avz._lib.lib
 lib.avz_debug_set_stamps.argtypes = [ct.c_void_p]
 for _ in range(3):
