@@ -1,0 +1,83 @@
+"""GPU tests of the reference-surface mirrors (oracle_debug.main, masked_mvdr.main,
+batch_run.run_batch) end to end through the C ABI, against the goldens / oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, triple_f32
+from oracle import avz_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _write_triple(d, name, mix_name="mixture.wav", tgt_name="target_reference.wav",
+                  int_name="interference_reference.wav"):
+    from avz import wavio
+    g = golden(f"inputs_{name}.npz")
+    os.makedirs(d, exist_ok=True)
+    wavio.write(os.path.join(d, mix_name), g["mix"] / 32768.0, 16000)
+    if tgt_name:
+        wavio.write(os.path.join(d, tgt_name), g["tgt"] / 32768.0, 16000)
+        wavio.write(os.path.join(d, int_name), g["int"] / 32768.0, 16000)
+
+
+def test_oracle_debug_main_mirror(gpu_device, tmp_path):
+    from avz import oracle_debug
+    outdir = str(tmp_path / oracle_debug.OUTDIR)
+    _write_triple(outdir, "test")
+    s_out = oracle_debug.main(outdir)          # shipped settings: 512/256, sigma 1
+    g = golden("full_test_n512_s1.npz")
+    assert len(s_out) == int(g["out_len"])
+    assert np.max(np.abs(s_out[::16] - g["out_stride16"])) <= 1e-4
+    assert os.path.exists(os.path.join(outdir, "output_oracle.wav"))
+    _, tgt, itf = triple_f32("test")
+    L = len(tgt)
+    assert abs(O.projection_sdr_sir(s_out[:L].astype(np.float64), tgt, itf)[1]
+               - float(g["sir_out"])) <= 0.01
+
+
+def test_masked_mvdr_main_mirror(gpu_device, tmp_path):
+    from avz import masked_mvdr
+    world = str(tmp_path / "run" / "World_Outputs")
+    _write_triple(world, "set2", mix_name="mixture_3_sources.wav", tgt_name=None)
+    s_out = masked_mvdr.main(world)
+    g = golden("ipd_set2_n512.npz")
+    assert len(s_out) == int(g["out_len"])
+    assert np.max(np.abs(s_out[::16] - g["out_stride16"])) <= 1e-4
+    assert os.path.exists(str(tmp_path / "run" / "MVDR_Outputs" / "output_masked_mvdr.wav"))
+
+
+def test_ipd_mask_helper_matches_reference_semantics(gpu_device):
+    from avz import masked_mvdr
+    mix, _, _ = triple_f32("test", (0, 20000))
+    _, _, Y = O.stft(mix, nperseg=512, noverlap=256)
+    m = masked_mvdr.compute_hard_geometric_mask(Y).cpu().numpy()
+    np.testing.assert_array_equal(m, O.ipd_mask_noise(Y))
+
+
+def test_device_metrics_match_host(gpu_device):
+    from avz import metrics
+    g = golden("metrics_vectors.npz")
+    o, t, i = (torch.from_numpy(g[k])[None].to(gpu_device) for k in ("o", "t", "i"))
+    _, sir = metrics.calculate_metrics_manual(o, t, i)
+    _, osir = metrics.calculate_osnr_osir(o, t, i)
+    assert abs(float(sir[0]) - float(g["sir"])) < 1e-9
+    assert abs(float(osir[0]) - float(g["osir"])) < 1e-9
+
+
+def test_batch_run_gpu_matches_oracle_enhancer(gpu_device):
+    from avz import batch_run
+
+    def oracle_enhance(mix, tgt, itf):
+        outs = [O.oracle_debug_vec(m.cpu().numpy(), t.cpu().numpy(), i.cpu().numpy(),
+                                   n_fft=1024, hop=512, sigma=1.0)
+                for m, t, i in zip(mix, tgt, itf)]
+        return torch.from_numpy(np.stack(outs)).to(mix.device)
+
+    gpu = batch_run.run_batch(6, start_idx=11, seconds=1.0, batch=4, device=gpu_device)
+    ref = batch_run.run_batch(6, start_idx=11, seconds=1.0, batch=4, device=gpu_device,
+                              enhance=oracle_enhance)
+    assert gpu.sums[4] == 6
+    np.testing.assert_allclose(gpu.sums[:4] / 6, ref.sums[:4] / 6, atol=0.01)  # mean dB
