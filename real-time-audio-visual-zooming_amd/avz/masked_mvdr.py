@@ -43,7 +43,8 @@ def compute_hard_geometric_mask(Y_stft, freqs=None):
         Y = Y.cuda()
     Y = Y.to(torch.complex64)
     pd = torch.angle(Y[0]) - torch.angle(Y[1])
-    return torch.where(pd.abs() > 0, 1.0, 0.01).to(torch.float64)
+    one = torch.ones((), dtype=torch.float64, device=Y.device)
+    return torch.where(pd.abs() > 0, one, 0.01 * one)
 
 
 def enhance(y_mix: np.ndarray, n_fft=N_FFT, sigma=SIGMA, d=D, device="cuda") -> np.ndarray:
