@@ -2,9 +2,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/avz.h"
 #include "avz_internal.h"
@@ -13,8 +15,19 @@ struct avz_plan {
   avz_config cfg;
   double tau1, tau2;         // far-field delays of the two mics (masked_mvdr.py:28-29)
   int max_frames;
-  uint8_t* maskbits;         // [max_batch][ceil(max_frames/4)][F] IBM nibbles
+  uint8_t* maskbits;         // [max_batch][ceil(max_frames/4)][F] IBM nibbles (fused path)
   long long mb_stride;
+  // chunked path workspace, one allocation (see avz_internal.h FusedArgs)
+  int nchunk;
+  void* arena;
+  float* part;
+  uint32_t* mwords;
+  double* steer;             // [F][4] steering vectors (masked_mvdr.py:22-35), fp64
+  float* coef;               // [max_batch][F][4] per-bin apply coefficients
+  float* heads;
+  float* tails;
+  uint32_t* peak_u;
+  bool use_fused;            // AVZ_KERNEL_PATH=fused selects the one-block-per-utterance kernel
 };
 
 static thread_local std::string g_last_hip;
@@ -77,6 +90,52 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
       return hip_fail(e);
     }
   }
+  {
+    const int H = c.n_fft / 2;
+    const long long B = c.max_batch;
+    p->nchunk = (p->max_frames + avz_chunk_frames() - 1) / avz_chunk_frames();
+    auto up = [](size_t n) { return (n + 255) & ~size_t(255); };
+    const size_t sz_part = up(sizeof(float) * B * p->nchunk * 5 * F);
+    const size_t sz_mw = up(sizeof(uint32_t) * B * p->nchunk * F);
+    const size_t sz_steer = up(sizeof(double) * F * 4);
+    const size_t sz_coef = up(sizeof(float) * B * F * 4);
+    const size_t sz_ht = up(sizeof(float) * B * p->nchunk * H);
+    const size_t sz_b = up(sizeof(uint32_t) * B);
+    hipError_t e = hipMalloc(&p->arena, sz_part + sz_mw + sz_steer + sz_coef + 2 * sz_ht + sz_b);
+    if (e != hipSuccess) {
+      if (p->maskbits) (void)hipFree(p->maskbits);
+      delete p;
+      return hip_fail(e);
+    }
+    char* q = static_cast<char*>(p->arena);
+    p->part = reinterpret_cast<float*>(q); q += sz_part;
+    p->mwords = reinterpret_cast<uint32_t*>(q); q += sz_mw;
+    p->steer = reinterpret_cast<double*>(q); q += sz_steer;
+    p->coef = reinterpret_cast<float*>(q); q += sz_coef;
+    p->heads = reinterpret_cast<float*>(q); q += sz_ht;
+    p->tails = reinterpret_cast<float*>(q); q += sz_ht;
+    p->peak_u = reinterpret_cast<uint32_t*>(q);
+    // d_m(f_k) = exp(-1j * (2 pi f_k) * tau_m), f_k = np.fft.rfftfreq(n_fft, 1/fs)[k]
+    std::vector<double> st((size_t)F * 4);
+    const double df = 1.0 / (c.n_fft * (1.0 / c.fs));
+    for (int k = 0; k < F; ++k) {
+      const double omega = 2 * M_PI * (k * df);
+      const double x1 = -omega * p->tau1, x2 = -omega * p->tau2;
+      st[4 * k + 0] = std::cos(x1);
+      st[4 * k + 1] = std::sin(x1);
+      st[4 * k + 2] = std::cos(x2);
+      st[4 * k + 3] = std::sin(x2);
+    }
+    e = hipMemcpy(p->steer, st.data(), sizeof(double) * st.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(p->arena);
+      if (p->maskbits) (void)hipFree(p->maskbits);
+      delete p;
+      return hip_fail(e);
+    }
+    const char* path = std::getenv("AVZ_KERNEL_PATH");
+    p->use_fused = path && std::strcmp(path, "fused") == 0;
+  }
   *out = p;
   return AVZ_OK;
 }
@@ -84,6 +143,7 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
 extern "C" int avz_plan_destroy(avz_plan* p) {
   if (!p) return AVZ_ERR_ARG;
   if (p->maskbits) (void)hipFree(p->maskbits);
+  if (p->arena) (void)hipFree(p->arena);
   delete p;
   return AVZ_OK;
 }
@@ -148,7 +208,17 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   k.norm_eps = (float)c.norm_eps;
   k.postfilter = c.postfilter;
   k.normalize = c.normalize;
-  const int rc = avz_launch_fused(c.n_fft, c.mask_mode, &k, stream);
+  k.max_frames = T;
+  k.nchunk = p->nchunk;
+  k.part = p->part;
+  k.mwords = p->mwords;
+  k.steer = p->steer;
+  k.coef = p->coef;
+  k.heads = p->heads;
+  k.tails = p->tails;
+  k.peak_u = p->peak_u;
+  const int rc = p->use_fused ? avz_launch_fused(c.n_fft, c.mask_mode, &k, stream)
+                              : avz_launch_chunked(c.n_fft, c.mask_mode, &k, stream);
   if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
   return rc;
 }

@@ -1,0 +1,663 @@
+// avz_chunked.hip — chunk-parallel form of the mask-driven MVDR chain (gfx950).
+//
+// An utterance's frames are cut into 32-frame chunks; each (chunk, utterance) pair is
+// one 256-thread (4-wave) workgroup, two per CU, so a batch of B utterances of T
+// frames launches B * ceil(T / 32) independent blocks instead of B long ones.
+//
+//   analysis   frames -> window -> FFT (mic pair / reference pair packed) -> LDS;
+//              thread-per-bin masks (IBM / IPD / external) and masked 2x2 covariance
+//              partials over the chunk (fp32) -> part[b][c][5][F]; IBM bits -> mwords.
+//   solve      one thread per (utterance, bin): partials summed in fp64, closed-form
+//              2x2 MVDR with the plan's steering table -> coef[b][k] (alpha, beta).
+//   synthesis  frames -> FFT again -> apply w^H y +
+//              post-filter -> two frames packed per inverse FFT -> windowed OLA of the
+//              chunk's 31 interior segments -> out; the chunk's first / last
+//              half-frame contributions -> heads/tails;
+//              block max |out| -> atomicMax(peak_u[b]).
+//   finalize   chunk-boundary segments (tails[c-1] + heads[c]), utterance peak,
+//              optional in-place peak normalisation of the chunk's segments.
+//
+// Reference semantics as avz_kernels.hip: rt_av_zoom/core/oracle_debug.py:27-97,
+// rt_av_zoom/core/masked_mvdr.py:50-132,
+// rt_av_zoom/core/full_audio_generating_pipeline/inference.py:88-118.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "avz_common.hpp"
+
+namespace avz {
+
+constexpr int kChunk = 32;      // frames per chunk = bits of one mask word
+constexpr int kCThreads = 256;  // 4 waves
+
+template <int N>
+struct CGeo {
+  using C = KCfg<N>;
+  static constexpr int NT = kCThreads;
+  static constexpr int NWAVE = NT / 64;
+  static constexpr int H = N / 2;
+  static constexpr int F = N / 2 + 1;
+  static constexpr int NSLOT = NWAVE * C::FPW;     // 8 frame slots
+  static constexpr int BPT = (N / 2) / NT;          // bins k < N/2 per thread
+  static constexpr int SLOT_LDS = NWAVE * C::WAVE_BYTES;
+  static constexpr int TW_OFF = SLOT_LDS;
+  static constexpr int MISC_OFF = TW_OFF + C::TW_BYTES;
+  static constexpr int LDS_BYTES = MISC_OFF + 64;
+  static_assert(BPT >= 1 && BPT * NT == N / 2, "bin mapping");
+  static_assert(2 * LDS_BYTES <= 160 * 1024, "two blocks per CU");
+};
+
+// Per-lane analysis window * 1/sum(win) and synthesis window * sum(win)/N terms.
+template <int N>
+struct WinCoef {
+  float a0, ac, as, s0, sc, ss;
+  __device__ __forceinline__ void init(const LaneMap<N>& lm) {
+    double s, c;
+    sincospi(2.0 * lm.in0 / N, &s, &c);
+    const double sca = 2.0 / N;
+    a0 = (float)(0.5 * sca);
+    ac = (float)(0.5 * sca * c);
+    as = (float)(0.5 * sca * s);
+    sincospi(2.0 * lm.out0 / N, &s, &c);
+    s0 = 0.25f;
+    sc = (float)(0.25 * c);
+    ss = (float)(0.25 * s);
+  }
+};
+
+// 1 / (win[m]^2 + win[m + N/2]^2): the istft window-sum normalisation of one sample.
+template <int N>
+__device__ __forceinline__ float inv_wsum(int m) {
+  const float c1 = cospif(2.0f * (float)m / (float)N);
+  const float wa = 0.5f - 0.5f * c1, wb = 0.5f + 0.5f * c1;
+  return 1.0f / (wa * wa + wb * wb);
+}
+
+template <int N>
+__device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<N>& wc,
+                                           const typename KCfg<N>::Fft& fft, cf* spec,
+                                           const cf* twid, const LaneMap<N>& lm) {
+  using C = KCfg<N>;
+  static_for<0, C::PPL>([&](auto r) {
+    constexpr int j = (C::IN_STRIDE * 32 / N) * r;  // 2 pi (IN_STRIDE r)/N = 2 pi j/32
+    constexpr float cr = W32::c[j % 32], sr = -W32::s[j % 32];
+    const float w = fmaf(wc.as, sr, fmaf(-wc.ac, cr, wc.a0));
+    v[r] = c_scale(v[r], w);
+  });
+  fft.forward(v, spec, twid);
+  static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
+}
+
+// Mask value m and covariance weight of one (bin, frame).
+template <int MASK>
+__device__ __forceinline__ float bin_mask(const FusedArgs& A, int b, cf x0, cf x1, cf zr,
+                                          cf zrp, int k, int t, bool& noise, float& wgt) {
+  if constexpr (MASK == MASK_IBM) {
+    // 2T = zr + conj(zrp), 2I = (zr - conj zrp)/i ; |2I|^2 > |2T|^2 <=> |I| > |T|
+    const float tr = zr.x + zrp.x, ti = zr.y - zrp.y;
+    const float ir = zr.y + zrp.y, ii = zr.x - zrp.x;
+    noise = ir * ir + ii * ii > tr * tr + ti * ti;
+    wgt = noise ? 1.0f : 0.0f;
+    return wgt;
+  } else if constexpr (MASK == MASK_IPD) {
+    wgt = ipd_weight(x0, x1);
+    return wgt;
+  } else {
+    const float M =
+        A.ext_mask[(long long)b * A.mask_sb + (long long)k * A.mask_sf + (long long)t * A.mask_st];
+    const float m = 1.0f - M;
+    wgt = m + A.weight_eps;
+    return m;
+  }
+}
+
+// ================================ analysis ================================
+template <int N, int MASK>
+__global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(FusedArgs A) {
+  using C = KCfg<N>;
+  using G = CGeo<N>;
+  constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
+  constexpr int FB = (MASK == MASK_IBM) ? NSLOT / 2 : NSLOT;  // frames per step
+  static_assert(kChunk % FB == 0, "steps tile the chunk");
+
+  extern __shared__ __align__(16) unsigned char lds[];
+  cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
+  C::Fft::fill_twiddles(twid, threadIdx.x, NT);
+
+  const int c = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int L = A.len[b];
+  if (L < N) return;  // host validates; finalize reports NaN for a bad device length
+  const int T = (L + H - 1) / H + 1;
+  const int nch = (T + kChunk - 1) / kChunk;
+  if (c >= nch) return;
+  if (c == 0 && tid == 0) A.peak_u[b] = 0u;
+  const int t0 = c * kChunk;
+  const int nframes = min(kChunk, T - t0);
+  const int nstep = (nframes + FB - 1) / FB;
+
+  typename C::Fft fft;
+  fft.init(lane);
+  LaneMap<N> lm;
+  lm.init(lane);
+  WinCoef<N> wc;
+  wc.init(lm);
+  const int my_slot = wave * C::FPW + lm.grp;
+  cf* my_spec = slot_ptr<N>(lds, my_slot);
+  // IBM: waves 0-1 transform the mic pair, waves 2-3 the reference pair (wave-uniform)
+  const bool ref = (MASK == MASK_IBM) && (wave * C::FPW >= FB);
+  const int my_frame = ref ? my_slot - FB : my_slot;
+  const int wave_frame0 = ref ? wave * C::FPW - FB : wave * C::FPW;
+
+  const float* mixb = A.mix + (long long)b * A.mix_stride;
+  rsrc_t r_re = make_rsrc(mixb, L), r_im = make_rsrc(mixb + A.ch_stride, L);
+  if constexpr (MASK == MASK_IBM) {
+    if (ref) {
+      r_re = make_rsrc(A.ref_tgt + (long long)b * A.ref_stride, L);
+      r_im = make_rsrc(A.ref_int + (long long)b * A.ref_stride, L);
+    }
+  }
+  cf v[PPL];
+  auto issue_loads = [&](int step) {
+    const int s0 = (t0 + step * FB + my_frame) * H - N / 2 + lm.in0;
+    static_for<0, PPL>([&](auto r) {
+      v[r].x = bload(r_re, s0 + C::IN_STRIDE * r);
+      v[r].y = bload(r_im, s0 + C::IN_STRIDE * r);
+    });
+  };
+
+  Acc32 acc[BPT];
+  uint32_t bits[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    acc[j].zero();
+    bits[j] = 0u;
+  }
+  // Nyquist bin N/2: frame `lane` of each step on the last wave's lanes.
+  const bool nyq_wave = (wave == G::NWAVE - 1);
+  Acc32 an;
+  an.zero();
+  uint32_t nyq_bits = 0u;
+
+  AVZ_STAMP_DECL();
+  issue_loads(0);
+  lds_barrier();  // twiddle table
+  AVZ_STAMP_INIT();
+  for (int step = 0; step < nstep; ++step) {
+    const int f0 = t0 + step * FB;
+    const bool live = f0 + wave_frame0 < T;  // wave-uniform: any of its frames exist
+#ifdef AVZ_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    AVZ_STAMP(0);
+#endif
+    if (live) window_fft<N>(v, wc, fft, my_spec, twid, lm);
+    if (step + 1 < nstep) issue_loads(step + 1);
+    lds_barrier();
+    AVZ_STAMP(1);
+    const int nvalid = min(FB, T - f0);
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int kb = tid + j * NT;
+      const int kp = (N - kb) & (N - 1);
+#pragma unroll
+      for (int i = 0; i < FB; ++i) {
+        if (i < nvalid) {
+          const cf* Zm = slot_ptr<N>(lds, i);
+          cf x0, x1, zr{0, 0}, zrp{0, 0};
+          split_pair(Zm[kb], Zm[kp], x0, x1);
+          if constexpr (MASK == MASK_IBM) {
+            const cf* Zr = slot_ptr<N>(lds, FB + i);
+            zr = Zr[kb];
+            zrp = Zr[kp];
+          }
+          bool noise = false;
+          float wgt;
+          const float m = bin_mask<MASK>(A, b, x0, x1, zr, zrp, kb, f0 + i, noise, wgt);
+          bits[j] |= (noise ? 1u : 0u) << (step * FB + i);
+          acc[j].add(x0, x1, wgt, m);
+        }
+      }
+    }
+    if (nyq_wave) {
+      bool noise = false;
+      if (lane < nvalid) {
+        const cf* Zm = slot_ptr<N>(lds, lane);
+        cf y0, y1, zr{0, 0};
+        split_pair(Zm[N / 2], Zm[N / 2], y0, y1);
+        if constexpr (MASK == MASK_IBM) zr = slot_ptr<N>(lds, FB + lane)[N / 2];
+        float wn;
+        const float mn = bin_mask<MASK>(A, b, y0, y1, zr, zr, N / 2, f0 + lane, noise, wn);
+        an.add(y0, y1, wn, mn);
+      }
+      const unsigned long long bal = __ballot(noise);
+      nyq_bits |= ((uint32_t)bal & ((1u << FB) - 1u)) << (step * FB);
+    }
+    lds_barrier();
+    AVZ_STAMP(2);
+  }
+
+  // ---- chunk partials
+  float* P = A.part + ((long long)b * A.nchunk + c) * 5 * F;
+  uint32_t* MW = A.mwords + ((long long)b * A.nchunk + c) * F;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int kb = tid + j * NT;
+    P[0 * F + kb] = acc[j].c00;
+    P[1 * F + kb] = acc[j].c11;
+    P[2 * F + kb] = acc[j].c01r;
+    P[3 * F + kb] = acc[j].c01i;
+    P[4 * F + kb] = acc[j].cm;
+    if constexpr (MASK == MASK_IBM) MW[kb] = bits[j];
+  }
+  if (nyq_wave) {
+    for (int o = 1; o < 64; o <<= 1) {
+      an.c00 += __shfl_xor(an.c00, o, 64);
+      an.c11 += __shfl_xor(an.c11, o, 64);
+      an.c01r += __shfl_xor(an.c01r, o, 64);
+      an.c01i += __shfl_xor(an.c01i, o, 64);
+      an.cm += __shfl_xor(an.cm, o, 64);
+    }
+    if (lane == 0) {
+      P[0 * F + N / 2] = an.c00;
+      P[1 * F + N / 2] = an.c11;
+      P[2 * F + N / 2] = an.c01r;
+      P[3 * F + N / 2] = an.c01i;
+      P[4 * F + N / 2] = an.cm;
+      if constexpr (MASK == MASK_IBM) MW[N / 2] = nyq_bits;
+    }
+  }
+
+}
+
+// ================================ solve ================================
+// One thread per (utterance, bin): sum the chunk partials in fp64, closed-form MVDR
+// with the plan's steering table -> coef[b][k] (+ optional cov/w debug outputs).
+constexpr int kSolveThreads = 256;
+
+template <int N>
+__global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(FusedArgs A) {
+  constexpr int H = N / 2, F = N / 2 + 1;
+  const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
+  if (idx >= (long long)A.batch * F) return;
+  const int b = (int)(idx / F), k = (int)(idx % F);
+  const int L = A.len[b];
+  if (L < N) return;
+  const int T = (L + H - 1) / H + 1;
+  const int nch = (T + kChunk - 1) / kChunk;
+  const float* P = A.part + (long long)b * A.nchunk * 5 * F + k;
+  double R[5] = {0, 0, 0, 0, 0};
+  for (int cc = 0; cc < nch; ++cc) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) R[q] += (double)P[((long long)cc * 5 + q) * F];
+  }
+  const double* d = A.steer + 4 * k;
+  cf al, be;
+  mvdr_solve_d(R, k, N, A, d[0], d[1], d[2], d[3], al, be,
+               A.w_out ? A.w_out + ((long long)b * F + k) * 4 : nullptr);
+  reinterpret_cast<float4*>(A.coef)[(long long)b * F + k] = make_float4(al.x, al.y, be.x, be.y);
+  if (A.cov_out) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) A.cov_out[((long long)b * F + k) * 5 + q] = R[q];
+  }
+}
+
+// ================================ synthesis ================================
+template <int N, int PF>
+__global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(FusedArgs A) {
+  using C = KCfg<N>;
+  using G = CGeo<N>;
+  constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
+  constexpr int FB = NSLOT;           // frames per step
+  constexpr int NPAIR = FB / 2;       // packed inverse FFTs per step
+  constexpr int M4 = H / 4;           // float4 groups per half frame
+  constexpr int NSG = NT / M4;        // segment groups
+  constexpr int SPT = FB / NSG;       // segments per thread per step
+  static_assert(SPT * NSG == FB, "OLA mapping");
+
+  extern __shared__ __align__(16) unsigned char lds[];
+  cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
+  float* red = reinterpret_cast<float*>(lds + G::MISC_OFF);
+  C::Fft::fill_twiddles(twid, threadIdx.x, NT);
+
+  const int c = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int L = A.len[b];
+  if (L < N) return;
+  const int T = (L + H - 1) / H + 1;
+  const int nch = (T + kChunk - 1) / kChunk;
+  if (c >= nch) return;
+  const int t0 = c * kChunk;
+  const int nstep = (min(kChunk, T - t0) + FB - 1) / FB;
+
+  typename C::Fft fft;
+  fft.init(lane);
+  LaneMap<N> lm;
+  lm.init(lane);
+  WinCoef<N> wc;
+  wc.init(lm);
+  const int my_slot = wave * C::FPW + lm.grp;
+  cf* my_spec = slot_ptr<N>(lds, my_slot);
+
+  const float* mixb = A.mix + (long long)b * A.mix_stride;
+  const rsrc_t r_m0 = make_rsrc(mixb, L), r_m1 = make_rsrc(mixb + A.ch_stride, L);
+  cf v[PPL];
+  auto issue_loads = [&](int step) {
+    const int s0 = (t0 + step * FB + my_slot) * H - N / 2 + lm.in0;
+    static_for<0, PPL>([&](auto r) {
+      v[r].x = bload(r_m0, s0 + C::IN_STRIDE * r);
+      v[r].y = bload(r_m1, s0 + C::IN_STRIDE * r);
+    });
+  };
+  AVZ_STAMP_DECL();
+  AVZ_STAMP_INIT();
+  issue_loads(0);
+
+  // ---- apply coefficients and post-filter bits of this thread's bins
+  const float4* coef = reinterpret_cast<const float4*>(A.coef) + (long long)b * F;
+  const uint32_t* MW = A.mwords + ((long long)b * A.nchunk + c) * F;
+  cf alpha[BPT], beta[BPT];
+  uint32_t bits[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const float4 cw = coef[tid + j * NT];
+    alpha[j] = cf{cw.x, cw.y};
+    beta[j] = cf{cw.z, cw.w};
+    bits[j] = (PF == PF_IBM_TARGET) ? MW[tid + j * NT] : 0u;
+  }
+  const bool nyq_wave = (wave == G::NWAVE - 1);
+  cf alpha_n{0, 0}, beta_n{0, 0};
+  uint32_t bits_n = 0u;
+  if (nyq_wave) {
+    const float4 cw = coef[N / 2];
+    alpha_n = cf{cw.x, cw.y};
+    beta_n = cf{cw.z, cw.w};
+    if (PF == PF_IBM_TARGET) bits_n = MW[N / 2];
+  }
+  auto gain = [&](uint32_t bb, int i, int t, int k) -> float {  // i: frame bit in chunk
+    if (t >= T) return 0.0f;
+    if constexpr (PF == PF_IBM_TARGET) {
+      return ((bb >> i) & 1u) ? 0.0f : 1.0f;
+    } else if constexpr (PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) {
+      const float M =
+          A.ext_mask[(long long)b * A.mask_sb + (long long)k * A.mask_sf + (long long)t * A.mask_st];
+      return PF == PF_EXT_FLOOR ? fmaxf(M, A.pf_floor) : M;
+    } else {
+      return 1.0f;
+    }
+  };
+
+  // OLA role: 4 consecutive samples m0.. of segments sgrp + NSG si
+  const int m0 = 4 * (tid % M4);
+  const int sgrp = tid / M4;
+  float inv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(m0 + i);
+  float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);  // previous frame's second half (sgrp 0)
+  float* outb = A.out + (long long)b * A.out_stride;
+  float peak = 0.0f;
+  const bool ifft_wave = wave < NPAIR / C::FPW;  // N = 512: waves holding a pair
+  float wi_c = 0.f, wi_s = 0.f;  // N = 1024 inverse: 0.25 cos / sin(2 pi n0 / N), x1 layout
+  if constexpr (N == 1024) {
+    double sn, cs;
+    sincospi(2.0 * ((lane & 31) + 512 * (lane >> 5)) / N, &sn, &cs);
+    wi_c = (float)(0.25 * cs);
+    wi_s = (float)(0.25 * sn);
+  }
+
+  lds_barrier();  // twiddle table
+  AVZ_STAMP(4);
+  for (int step = 0; step < nstep; ++step) {
+    const int f0 = t0 + step * FB;
+    const bool more = step + 1 < nstep;
+#ifdef AVZ_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    AVZ_STAMP(5);
+#endif
+    window_fft<N>(v, wc, fft, my_spec, twid, lm);
+    if (more) issue_loads(step + 1);  // in flight through apply, inverse FFT and OLA
+    lds_barrier();
+    AVZ_STAMP(6);
+
+    // ---- apply w^H y and the post-filter; pack frames (2p, 2p+1) into slot 2p
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int kb = tid + j * NT;
+      const int kp = (N - kb) & (N - 1);
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p) {
+        const int ta = f0 + 2 * p;
+        if (ta < T) {
+          cf* Za = slot_ptr<N>(lds, 2 * p);
+          const cf* Zb = slot_ptr<N>(lds, 2 * p + 1);
+          const int ia = step * FB + 2 * p;
+          const float ga = gain(bits[j], ia, ta, kb), gb = gain(bits[j], ia + 1, ta + 1, kb);
+          const cf za = Za[kb], zap = Za[kp], zb = Zb[kb], zbp = Zb[kp];
+          const cf sa = apply_bin(alpha[j], beta[j], za, zap, ga);
+          const cf sb = apply_bin(alpha[j], beta[j], zb, zbp, gb);
+          Za[kp] = {sa.x + sb.y, sb.x - sa.y};  // conj(Sa) + i conj(Sb) at N - k
+          // Sa + i Sb at k; at DC irfft keeps only the real parts (written last: kp == kb)
+          Za[kb] = (kb == 0) ? cf{sa.x, sb.x} : cf{sa.x - sb.y, sa.y + sb.x};
+        }
+      }
+    }
+    if (nyq_wave && lane < NPAIR) {  // Nyquist bin: frame pair `lane`
+      const int ta = f0 + 2 * lane;
+      if (ta < T) {
+        const int ia = step * FB + 2 * lane;
+        cf* Za = slot_ptr<N>(lds, 2 * lane);
+        const cf* Zb = slot_ptr<N>(lds, 2 * lane + 1);
+        const float ga = gain(bits_n, ia, ta, N / 2), gb = gain(bits_n, ia + 1, ta + 1, N / 2);
+        const cf za = Za[N / 2], zb = Zb[N / 2];
+        Za[N / 2] = {apply_bin(alpha_n, beta_n, za, za, ga).x,
+                     apply_bin(alpha_n, beta_n, zb, zb, gb).x};
+      }
+    }
+    lds_barrier();
+    AVZ_STAMP(7);
+
+    // ---- inverse FFT of the packed pairs -> windowed frame contributions in slot 2p+1
+    if constexpr (N == 1024) {
+      // four pairs, four waves: one 64-lane 1024-point transform each (x1 layout:
+      // output register k of lane (l, h) is sample l + 512 h + 32 k)
+      cf u[16];
+      cf* Zi = slot_ptr<N>(lds, 2 * wave);
+      static_for<0, 16>([&](auto r) { u[r] = c_conj(Zi[64 * r + lane]); });
+      Fft1024::forward_tw(u, Zi, twid, lane);
+      float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * wave + 1));
+      const int n0 = (lane & 31) + 512 * (lane >> 5);
+      static_for<0, 16>([&](auto k) {
+        constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+        const float w = fmaf(wi_s, sk, fmaf(-wi_c, ck, 0.25f));
+        const int n = n0 + 32 * k;
+        Cp[n] = u[k].x * w;       // frame 2p   (real part of the inverse)
+        Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
+      });
+    } else if (ifft_wave) {
+      const int p = wave * C::FPW + lm.grp;
+      cf* Zi = slot_ptr<N>(lds, 2 * p);
+      cf u[PPL];
+      static_for<0, PPL>([&](auto r) { u[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
+      fft.forward(u, Zi, twid);
+      float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
+      static_for<0, PPL>([&](auto k) {
+        constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+        const float w = fmaf(wc.ss, sk, fmaf(-wc.sc, ck, wc.s0));
+        const int n = lm.out0 + C::OUT_STRIDE * k;
+        Cp[n] = u[k].x * w;       // frame 2p   (real part of the inverse)
+        Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
+      });
+    }
+    lds_barrier();
+    AVZ_STAMP(8);
+
+    // ---- overlap-add: segment j = f0 - 1 + s = frame s-1 (2nd half) + frame s (1st half)
+    auto cframe = [&](int f) -> const float* {
+      return reinterpret_cast<const float*>(slot_ptr<N>(lds, 2 * (f >> 1) + 1)) + (f & 1) * N;
+    };
+#pragma unroll
+    for (int si = 0; si < SPT; ++si) {
+      const int s = sgrp + si * NSG;
+      const float4 vb = *reinterpret_cast<const float4*>(cframe(s) + m0);
+      if (s == 0 && step == 0) {  // chunk's first frame: finalize adds the previous tail
+        *reinterpret_cast<float4*>(A.heads + ((long long)b * A.nchunk + c) * H + m0) = vb;
+        continue;
+      }
+      const int j = f0 - 1 + s;
+      if (j <= T - 2) {
+        const float4 va =
+            (s == 0) ? carry : *reinterpret_cast<const float4*>(cframe(s - 1) + H + m0);
+        float4 o;
+        o.x = (va.x + vb.x) * inv[0];
+        o.y = (va.y + vb.y) * inv[1];
+        o.z = (va.z + vb.z) * inv[2];
+        o.w = (va.w + vb.w) * inv[3];
+        *reinterpret_cast<float4*>(outb + (long long)j * H + m0) = o;
+        peak = fmaxf(peak, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+      }
+    }
+    if (sgrp == 0) carry = *reinterpret_cast<const float4*>(cframe(FB - 1) + H + m0);
+    lds_barrier();
+    AVZ_STAMP(9);
+  }
+  if (sgrp == 0 && nstep * FB == kChunk)  // full chunk: its last frame's tail
+    *reinterpret_cast<float4*>(A.tails + ((long long)b * A.nchunk + c) * H + m0) = carry;
+
+  // ---- block max |out| -> utterance running max (non-negative floats order as uints)
+  for (int o = 32; o > 0; o >>= 1) peak = fmaxf(peak, __shfl_xor(peak, o, 64));
+  if (lane == 0) red[wave] = peak;
+  __syncthreads();
+  if (tid == 0) {
+    float pk = red[0];
+#pragma unroll
+    for (int w = 1; w < G::NWAVE; ++w) pk = fmaxf(pk, red[w]);
+    atomicMax(A.peak_u + b, __float_as_uint(pk));
+  }
+  AVZ_STAMP(10);
+}
+
+// ================================ finalize ================================
+template <int N>
+__global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(FusedArgs A) {
+  constexpr int NT = kCThreads, H = N / 2, NWAVE = NT / 64;
+  __shared__ float red[NWAVE];
+  const int c = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int L = A.len[b];
+  if (L < N) {
+    if (c == 0 && tid == 0 && A.peak) A.peak[b] = __builtin_nanf("");
+    return;
+  }
+  const int T = (L + H - 1) / H + 1;
+  const int nch = (T + kChunk - 1) / kChunk;
+  if (c >= nch) return;
+  const float* heads = A.heads + (long long)b * A.nchunk * H;
+  const float* tails = A.tails + (long long)b * A.nchunk * H;
+  // boundary segment 32 cc - 1 = tail(cc - 1) + head(cc), cc = 1 .. nch - 1
+  auto boundary = [&](int cc, int m) -> float {
+    return (tails[(long long)(cc - 1) * H + m] + heads[(long long)cc * H + m]) * inv_wsum<N>(m);
+  };
+  float pk = 0.0f;
+  for (int idx = tid; idx < (nch - 1) * H; idx += NT)
+    pk = fmaxf(pk, fabsf(boundary(idx / H + 1, idx % H)));
+  for (int o = 32; o > 0; o >>= 1) pk = fmaxf(pk, __shfl_xor(pk, o, 64));
+  if (lane == 0) red[wave] = pk;
+  __syncthreads();
+  pk = __uint_as_float(A.peak_u[b]);
+#pragma unroll
+  for (int w = 0; w < NWAVE; ++w) pk = fmaxf(pk, red[w]);
+  if (c == 0 && tid == 0 && A.peak) A.peak[b] = pk;
+  const float scale = (A.normalize == NORM_PEAK) ? 1.0f / (pk + A.norm_eps) : 1.0f;
+  float* outb = A.out + (long long)b * A.out_stride;
+  if (c >= 1) {
+    const long long j = (long long)kChunk * c - 1;
+    for (int m = tid; m < H; m += NT) outb[j * H + m] = boundary(c, m) * scale;
+  }
+  if (A.normalize == NORM_PEAK) {  // the chunk's interior segments 32c .. 32c+30
+    const int j0 = kChunk * c, j1 = min(kChunk * c + kChunk - 1, T - 1);
+    float4* o4 = reinterpret_cast<float4*>(outb + (long long)j0 * H);
+    const int n4 = (j1 - j0) * H / 4;
+    for (int i = tid; i < n4; i += NT) {
+      float4 x = o4[i];
+      x.x *= scale; x.y *= scale; x.z *= scale; x.w *= scale;
+      o4[i] = x;
+    }
+  }
+}
+
+}  // namespace avz
+
+using namespace avz;
+
+extern "C" int avz_chunk_frames(void) { return kChunk; }
+
+#ifdef AVZ_STAMPS
+extern "C" int avz_debug_set_stamps_chunked(void* dev_ptr) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -3;
+}
+#endif
+
+template <typename K>
+static bool set_lds(K kern, int lds) {
+  return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) ==
+         hipSuccess;
+}
+
+template <int N, int MASK, int PF>
+static int launch_chunked_t(const FusedArgs* a, hipStream_t st) {
+  auto k1 = avz_analysis_kernel<N, MASK>;
+  auto k2 = avz_synthesis_kernel<N, PF>;
+  auto k3 = avz_finalize_kernel<N>;
+  auto ks = avz_solve_kernel<N>;
+  constexpr int lds = CGeo<N>::LDS_BYTES;
+  static bool attr_done = false;
+  if (!attr_done) {
+    if (!set_lds(k1, lds) || !set_lds(k2, lds)) return -3;
+    attr_done = true;
+  }
+  const int nch = (a->max_frames + kChunk - 1) / kChunk;
+  if (nch > a->nchunk) return -2;
+  const dim3 grid(nch, a->batch);
+  constexpr int F = N / 2 + 1;
+  const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
+  hipLaunchKernelGGL(k1, grid, dim3(kCThreads), lds, st, *a);
+  hipLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, *a);
+  hipLaunchKernelGGL(k2, grid, dim3(kCThreads), lds, st, *a);
+  hipLaunchKernelGGL(k3, grid, dim3(kCThreads), 0, st, *a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <int N, int MASK>
+static int launch_pf(const FusedArgs* a, hipStream_t st) {
+  if constexpr (MASK == MASK_IBM) {
+    if (a->postfilter == PF_IBM_TARGET) return launch_chunked_t<N, MASK, PF_IBM_TARGET>(a, st);
+  }
+  if constexpr (MASK == MASK_EXTERNAL) {
+    if (a->postfilter == PF_EXT_FLOOR) return launch_chunked_t<N, MASK, PF_EXT_FLOOR>(a, st);
+    if (a->postfilter == PF_EXT_MUL) return launch_chunked_t<N, MASK, PF_EXT_MUL>(a, st);
+  }
+  if (a->postfilter == PF_NONE) return launch_chunked_t<N, MASK, PF_NONE>(a, st);
+  return -4;
+}
+
+extern "C" int avz_launch_chunked(int n_fft, int mask_mode, const FusedArgs* a, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (a->batch <= 0) return 0;
+  if (n_fft == 1024) {
+    switch (mask_mode) {
+      case MASK_IBM: return launch_pf<1024, MASK_IBM>(a, st);
+      case MASK_IPD: return launch_pf<1024, MASK_IPD>(a, st);
+      case MASK_EXTERNAL: return launch_pf<1024, MASK_EXTERNAL>(a, st);
+    }
+  } else if (n_fft == 512) {
+    switch (mask_mode) {
+      case MASK_IBM: return launch_pf<512, MASK_IBM>(a, st);
+      case MASK_IPD: return launch_pf<512, MASK_IPD>(a, st);
+      case MASK_EXTERNAL: return launch_pf<512, MASK_EXTERNAL>(a, st);
+    }
+  }
+  return -4;
+}

@@ -221,6 +221,26 @@ struct Fft1024 {
     dft16(v);
     xhalf_dit<32>(v, sgn);
   }
+
+  // The same transform for a lane that did not init(): twiddles W1024^{l k1} come
+  // from a block-shared LDS table tw[k1 * 32 + l] (Fft1024x2::fill_twiddles).
+  __device__ __forceinline__ static void forward_tw(cf (&v)[16], cf* scratch, const cf* tw,
+                                                    int lane) {
+    const int l = lane & 31, h = lane >> 5;
+    const float sg = h ? -1.0f : 1.0f;
+    cf t[16];
+    static_for<0, 16>([&](auto k) { t[k] = tw[(k + 16 * h) * 32 + l]; });
+    __builtin_amdgcn_sched_barrier(0);  // twiddle reads in flight during the first DFT
+    dft16(v);
+    xhalf_dit<32>(v, sg);
+    static_for<0, 16>([&](auto k) { v[k] = c_mul(v[k], t[k]); });
+    static_for<0, 16>([&](auto k) { scratch[(k + 16 * h) * 33 + l] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = scratch[l * 33 + 2 * r + h]; });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<32>(v, sg);
+  }
 };
 
 // -------------------------------------------------------------------- Fft1024x2

@@ -30,6 +30,16 @@ struct FusedArgs {
   double fs, sigma, tau1, tau2, fmin_hz;
   float weight_eps, pf_floor, norm_eps;
   int postfilter, normalize;
+  // chunked path workspace (plan-owned)
+  int max_frames;             // frames of the longest utterance (grid extent)
+  int nchunk;                 // allocated 32-frame chunks per utterance (workspace stride)
+  float* part;                // [B][nchunk][5][F] masked covariance partials (fp32)
+  uint32_t* mwords;           // [B][nchunk][F] IBM bits, bit i = frame 32 c + i is noise
+  const double* steer;        // [F][4] steering vector d0 (re, im), d1 (re, im), fp64
+  float* coef;                // [B][F][4] apply coefficients alpha (re, im), beta (re, im)
+  float* heads;               // [B][nchunk][H] chunk's first frame, first-half contribution
+  float* tails;               // [B][nchunk][H] chunk's last frame, second-half contribution
+  uint32_t* peak_u;           // [B] max |out| over chunk interiors (float bits, atomicMax)
 };
 
 struct StftArgs {
@@ -46,6 +56,8 @@ struct StftArgs {
 
 extern "C" {
 int avz_launch_fused(int n_fft, int mask_mode, const avz::FusedArgs* a, void* stream);
+int avz_launch_chunked(int n_fft, int mask_mode, const avz::FusedArgs* a, void* stream);
+int avz_chunk_frames(void);
 int avz_launch_stft(int n_fft, const avz::StftArgs* a, void* stream);
 int avz_fused_lds_bytes(int n_fft);
 }

@@ -16,232 +16,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "avz_fft.hpp"
-#include "avz_internal.h"
+#include "avz_common.hpp"
 
 namespace avz {
-
-constexpr int kThreads = 1024;
-constexpr int kWaves = 16;
-
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-__device__ __forceinline__ rsrc_t make_rsrc(const float* p, long long n_floats) {
-  long long bytes = (p == nullptr || n_floats <= 0) ? 0 : n_floats * 4;
-  if (bytes > 0x7fffffffLL) bytes = 0x7fffffffLL;
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
-}
-
-__device__ __forceinline__ float bload(rsrc_t r, int elem) {
-  // Offsets >= the descriptor's byte length read 0: scipy's zero extension/padding.
-  // A negative index becomes the largest dword offset (always out of range) via a
-  // select, so no voffset + immediate split can depend on 32-bit wraparound.
-  const unsigned off = (elem < 0) ? 0xfffffffcu : (unsigned)elem * 4u;
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
-}
-
-// Diagnostic build only (-DAVZ_STAMPS): wave 0 accumulates s_memrealtime (100 MHz)
-// deltas per phase into g_stamps[block][16]. Phases: 0 pass-1 FFT (rest), 1 pass-1 bins,
-// 2 solve, 3 pass-2 FFT (rest), 4 pass-2 bins, 5 inverse FFT, 6 overlap-add,
-// 7 peak/normalise, 8 wait for prefetched samples, 9 FFT stage 1, 10 transpose,
-// 11 FFT stage 2 + spectrum store (8-11 summed over both passes, N = 1024 only).
-#ifdef AVZ_STAMPS
-__device__ unsigned long long* g_stamps;
-#define AVZ_STAMP_DECL() unsigned long long stamp_prev = 0
-#define AVZ_STAMP_INIT() stamp_prev = __builtin_amdgcn_s_memrealtime()
-#define AVZ_STAMP(i)                                                        \
-  do {                                                                      \
-    if (threadIdx.x == 0 && g_stamps) {                                     \
-      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();     \
-      g_stamps[blockIdx.x * 16 + (i)] += now_ - stamp_prev;                 \
-      stamp_prev = now_;                                                    \
-    }                                                                       \
-  } while (0)
-#else
-#define AVZ_STAMP_DECL() (void)0
-#define AVZ_STAMP_INIT() (void)0
-#define AVZ_STAMP(i) (void)0
-#endif
-
-// LDS-only barrier: leaves global loads (the next frame's prefetch) in flight.
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-template <int N>
-struct KCfg;
-template <>
-struct KCfg<1024> {
-  using Fft = Fft1024x2;
-  static constexpr int PPL = Fft::PPL;       // complex points per lane
-  static constexpr int FPW = 2;              // FFTs per wave (lane groups of 32)
-  static constexpr int GROUP_BYTES = 32 * 33 * 8;
-  static constexpr int WAVE_BYTES = 2 * GROUP_BYTES;
-  static constexpr int IN_STRIDE = 32;       // sample stride between registers
-  static constexpr int OUT_STRIDE = 32;      // bin/time stride between registers
-  static constexpr int TW_BYTES = 32 * 32 * 8;  // block-shared W1024^{l k1} table
-};
-template <>
-struct KCfg<512> {
-  using Fft = Fft512x2;
-  static constexpr int PPL = Fft::PPL;
-  static constexpr int FPW = 2;
-  static constexpr int GROUP_BYTES = 16 * 34 * 8;
-  static constexpr int WAVE_BYTES = 2 * GROUP_BYTES;
-  static constexpr int IN_STRIDE = 32;
-  static constexpr int OUT_STRIDE = 16;
-  static constexpr int TW_BYTES = 0;
-};
-
-template <int N, int NT = kThreads>
-struct Geo {
-  using C = KCfg<N>;
-  static constexpr int NWAVE = NT / 64;
-  static constexpr int H = N / 2;
-  static constexpr int NB = N / 2;          // bins per q-row (bin N/2 rides with k = 0)
-  static constexpr int F = N / 2 + 1;
-  static constexpr int Q = NT / NB;         // frame groups in the per-bin phase
-  static constexpr int NSLOT = NWAVE * C::FPW;
-  static constexpr int SLOT_LDS = NWAVE * C::WAVE_BYTES;
-  // LDS map: [FFT slots][OLA carry 2 x H f32][twiddles][Nyquist sums Q x 5 f64][2 coefs]
-  static constexpr int CARRY_OFF = SLOT_LDS;
-  static constexpr int TW_OFF = CARRY_OFF + 2 * H * 4;
-  static constexpr int NYQ_OFF = TW_OFF + C::TW_BYTES;
-  static constexpr int LDS_BYTES = NYQ_OFF + Q * 5 * 8 + 16;
-  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-  static_assert(NB * 5 * 8 * Q <= SLOT_LDS, "covariance reduction must fit the slot area");
-};
-
-template <int N>
-__device__ __forceinline__ cf* slot_ptr(unsigned char* lds, int s) {
-  using C = KCfg<N>;
-  return reinterpret_cast<cf*>(lds + (s / C::FPW) * C::WAVE_BYTES + (s % C::FPW) * C::GROUP_BYTES);
-}
-
-// Per-lane geometry of the wave FFT (input sample / output index of each register).
-template <int N>
-struct LaneMap {
-  int in0;    // input index of register 0 (lane part)
-  int grp;    // lane group (N=512: which of the two FFTs; N=1024: 0)
-  int out0;   // output index of register 0
-  __device__ __forceinline__ void init(int lane) {
-    if constexpr (N == 1024) {
-      in0 = lane & 31;
-      grp = lane >> 5;
-      out0 = lane & 31;
-    } else {
-      in0 = lane & 31;
-      grp = lane >> 5;
-      out0 = (lane & 15) + 256 * ((lane >> 4) & 1);
-    }
-  }
-};
-
-// a = (z + conj zp)/2, b = (z - conj zp)/(2i): split of a packed real pair.
-// Written so that a self-partnered bin (DC, Nyquist: zp == z) yields exact +0
-// imaginary parts, as pocketfft's r2c does (matters for the IPD angle test).
-__device__ __forceinline__ void split_pair(cf z, cf zp, cf& a, cf& b) {
-  a = {0.5f * (z.x + zp.x), 0.5f * (z.y - zp.y)};
-  b = {0.5f * (z.y + zp.y), 0.5f * (zp.x - z.x)};
-}
-// DC / Nyquist bins: both parts are real; imaginary parts are +0 (pocketfft r2c).
-__device__ __forceinline__ void split_self(cf z, cf& a, cf& b) {
-  a = {z.x, 0.0f};
-  b = {z.y, 0.0f};
-}
-
-// Heuristic phase mask (masked_mvdr.py:37-46): 0.01 where angle(Y0) == angle(Y1)
-// as float32, else 1.0. A cross-product test settles every bin whose angles differ
-// by far more than an fp32 ulp; the rest compare atan2f exactly.
-__device__ __forceinline__ float ipd_weight(cf a, cf b) {
-  const float cr = a.y * b.x - a.x * b.y;
-  const float n2 = (a.x * a.x + a.y * a.y) * (b.x * b.x + b.y * b.y);
-  if (cr * cr > 1e-10f * n2) return 1.0f;
-  const float pa = atan2f(a.y, a.x), pb = atan2f(b.y, b.x);
-  return (fabsf(pa - pb) > 0.0f) ? 1.0f : 0.01f;
-}
-
-struct Acc32 {
-  float c00, c11, c01r, c01i, cm;
-  __device__ __forceinline__ void zero() { c00 = c11 = c01r = c01i = cm = 0.f; }
-  __device__ __forceinline__ void add(cf x0, cf x1, float wgt, float m) {
-    c00 = fmaf(wgt, x0.x * x0.x + x0.y * x0.y, c00);
-    c11 = fmaf(wgt, x1.x * x1.x + x1.y * x1.y, c11);
-    c01r = fmaf(wgt, x0.x * x1.x + x0.y * x1.y, c01r);  // Re x0 conj(x1)
-    c01i = fmaf(wgt, x0.y * x1.x - x0.x * x1.y, c01i);  // Im x0 conj(x1)
-    cm += m;
-  }
-};
-struct Acc64 {
-  double c[5];
-  __device__ __forceinline__ void zero() {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) c[i] = 0.0;
-  }
-  __device__ __forceinline__ void add(const Acc32& a) {
-    c[0] += (double)a.c00;
-    c[1] += (double)a.c11;
-    c[2] += (double)a.c01r;
-    c[3] += (double)a.c01i;
-    c[4] += (double)a.cm;
-  }
-};
-
-// Per-bin MVDR solve in fp64 (oracle_debug.py:66-79):
-//   w~ = (R/(sum m + 1e-6) + sigma I)^{-1} d ; w = w~ / (d^H w~ + 1e-10);
-//   singular -> w = [1, 0]; f < fmin -> w = 0.
-// Returns the pass-2 apply coefficients S = alpha Z[k] + beta conj(Z[N-k]).
-__device__ __forceinline__ void mvdr_solve(const double (&c)[5], int k, int n_fft,
-                                           const FusedArgs& A, cf& alpha, cf& beta,
-                                           float* w_dbg) {
-  double w0r = 0, w0i = 0, w1r = 0, w1i = 0;
-  const double fk = (double)k * A.fs / (double)n_fft;
-  if (!(fk < A.fmin_hz)) {
-    const double nrm = c[4] + 1e-6;
-    const double a = c[0] / nrm + A.sigma, e = c[1] / nrm + A.sigma;
-    const double br = c[2] / nrm, bi = c[3] / nrm;
-    const double det = a * e - (br * br + bi * bi);
-    if (det == 0.0 || !isfinite(det)) {
-      w0r = 1.0;
-    } else {
-      const double om = 2.0 * M_PI * fk;
-      double s1, c1, s2, c2;
-      sincos(om * A.tau1, &s1, &c1);
-      sincos(om * A.tau2, &s2, &c2);
-      const double d0r = c1, d0i = -s1, d1r = c2, d1i = -s2;
-      // w~0 = (e d0 - b d1)/det ; w~1 = (a d1 - conj(b) d0)/det
-      double t0r = e * d0r - (br * d1r - bi * d1i);
-      double t0i = e * d0i - (br * d1i + bi * d1r);
-      double t1r = a * d1r - (br * d0r + bi * d0i);
-      double t1i = a * d1i - (br * d0i - bi * d0r);
-      t0r /= det; t0i /= det; t1r /= det; t1i /= det;
-      // den = conj(d0) w~0 + conj(d1) w~1 + 1e-10
-      const double dr = d0r * t0r + d0i * t0i + d1r * t1r + d1i * t1i + 1e-10;
-      const double di = d0r * t0i - d0i * t0r + d1r * t1i - d1i * t1r;
-      const double dd = dr * dr + di * di;
-      w0r = (t0r * dr + t0i * di) / dd;
-      w0i = (t0i * dr - t0r * di) / dd;
-      w1r = (t1r * dr + t1i * di) / dd;
-      w1i = (t1i * dr - t1r * di) / dd;
-    }
-  }
-  // alpha = (conj w0 - i conj w1)/2 ; beta = (conj w0 + i conj w1)/2
-  alpha = {(float)(0.5 * (w0r - w1i)), (float)(0.5 * (-w0i - w1r))};
-  beta = {(float)(0.5 * (w0r + w1i)), (float)(0.5 * (-w0i + w1r))};
-  if (w_dbg) {
-    w_dbg[0] = (float)w0r;
-    w_dbg[1] = (float)w0i;
-    w_dbg[2] = (float)w1r;
-    w_dbg[3] = (float)w1i;
-  }
-}
-
-__device__ __forceinline__ cf apply_bin(cf alpha, cf beta, cf z, cf zp, float g) {
-  const cf s = c_add(c_mul(alpha, z), c_mul(beta, c_conj(zp)));
-  return {g * s.x, g * s.y};
-}
 
 template <int N, int MASK, int NT>
 __global__ void __launch_bounds__(NT, 1) avz_fused_kernel(FusedArgs A) {

@@ -1,0 +1,29 @@
+"""FFT-phase throughput (FFTs per microsecond per CU) for several FFT shapes / wave
+counts. python tools/micro/fftbench.py (needs libfftbench.so next to it)."""
+import ctypes as ct
+import os
+import torch
+
+here = os.path.dirname(os.path.abspath(__file__))
+lib = ct.CDLL(os.path.join(here, "libfftbench.so"))
+lib.run_bench.argtypes = [ct.c_int, ct.c_void_p, ct.c_void_p, ct.c_int, ct.c_int]
+dev = torch.device("cuda")
+inp = torch.randn(1024, device=dev)
+out = torch.empty(1024 * 1024, device=dev)
+iters = 200
+names = {0: "x2 (32 pts/lane), 8 waves/block", 1: "x1 (16 pts/lane), 16 waves/block",
+         2: "x1 (16 pts/lane), 8 waves/block", 3: "x2, 4 waves/block (x2 blocks/CU)"}
+ffts_per_block = {0: 16, 1: 16, 2: 8, 3: 8}
+for v, blocks in ((0, 256), (1, 256), (2, 256), (3, 512), (2, 512)):
+    for _ in range(2):
+        lib.run_bench(v, inp.data_ptr(), out.data_ptr(), blocks, iters)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    assert lib.run_bench(v, inp.data_ptr(), out.data_ptr(), blocks, iters) == 0
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3
+    ffts = blocks * ffts_per_block[v] * iters
+    print(f"{names[v]:40s} blocks={blocks:4d}: {us:8.1f} us  {ffts / us / 256:6.2f} FFT/us/CU  "
+          f"({us / iters:.2f} us per phase)")

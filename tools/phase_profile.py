@@ -1,4 +1,4 @@
-"""Per-phase time breakdown of the fused kernel (diagnostic build libavz_stamps.so).
+"""Per-phase time breakdown of the MVDR kernels (diagnostic build libavz_stamps.so).
 
 Wave 0 of every block accumulates s_memrealtime (100 MHz) deltas between the
 kernel's barriers; this prints the mean per block in microseconds. The stamped build
@@ -21,7 +21,13 @@ import torch  # noqa: E402
 import avz  # noqa: E402
 from avz import synth  # noqa: E402
 
-PHASES = ["p1 FFT rest", "p1 bins", "solve", "p2 FFT rest", "p2 bins", "iFFT", "OLA", "peak/norm", "load wait", "fft stage1", "fft transp", "fft stage2"]
+FUSED = os.environ.get("AVZ_KERNEL_PATH") == "fused"
+if FUSED:  # avz_kernels.hip, one block per utterance
+    PHASES = ["p1 FFT rest", "p1 bins", "solve", "p2 FFT rest", "p2 bins", "iFFT", "OLA",
+              "peak/norm", "load wait", "fft stage1", "fft transp", "fft stage2"]
+else:  # avz_chunked.hip: analysis 0-3, synthesis 4-10, one block per (chunk, utterance)
+    PHASES = ["A load wait", "A FFT", "A bins", "A partials", "S prologue", "S load wait",
+              "S FFT", "S apply", "S iFFT", "S OLA", "S peak"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=256)
@@ -38,14 +44,16 @@ plan = avz.MVDRPlan(n_fft=a.n_fft, sigma=1.0, mic_d=0.01, mask=a.mask,
                     max_batch=a.batch, max_samples=S)
 d = [torch.from_numpy(x).to(dev) for x in (mix, tgt, itf)]
 kw = dict(ref_tgt=d[1], ref_int=d[2]) if a.mask == "ibm" else {}
-st = torch.zeros((a.batch, 16), dtype=torch.int64, device=dev)
+nblk = a.batch if FUSED else a.batch * -(-plan.frames(S) // avz._lib.lib.avz_chunk_frames())
+st = torch.zeros((nblk, 16), dtype=torch.int64, device=dev)
 lib = avz._lib.lib
-lib.avz_debug_set_stamps.argtypes = [ct.c_void_p]
+setter = lib.avz_debug_set_stamps if FUSED else lib.avz_debug_set_stamps_chunked
+setter.argtypes = [ct.c_void_p]
 for _ in range(3):
     plan.run(d[0], **kw)
 torch.cuda.synchronize()
 st.zero_()
-assert lib.avz_debug_set_stamps(ct.c_void_p(st.data_ptr())) == 0
+assert setter(ct.c_void_p(st.data_ptr())) == 0
 reps = 5
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
