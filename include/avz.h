@@ -41,6 +41,13 @@ extern "C" {
 #define AVZ_PF_EXT_FLOOR 2  /* x max(M, floor), full_audio.../inference.py:116           */
 #define AVZ_PF_EXT_MUL 3    /* x M, Final_pipeline/src/inference.py:219                  */
 
+/* beamformers (A8 / A14) */
+#define AVZ_BF_MVDR 0       /* (R/(sum m + 1e-6) + sigma I)^-1 d, normalised; oracle_debug.py:66-79 */
+#define AVZ_BF_HYBRID_NULL 1 /* principal eigenvector of the noise covariance as a hard null
+                               next to the phase-normalised target steering vector; delay-and-sum
+                               when cond([v_tgt, v_int]) > cond_max; mic 0 below bypass_hz;
+                               Final_pipeline/src/inference.py:16-98                          */
+
 /* output normalisation (A12) */
 #define AVZ_NORM_NONE 0     /* un-normalised; peak[] reports max|out|                     */
 #define AVZ_NORM_PEAK 1     /* out /= (max|out| + norm_eps), oracle_debug.py:94 (eps 0),
@@ -64,6 +71,10 @@ typedef struct avz_config {
   double norm_eps;   /* 0 (oracle_debug), 1e-6 (masked_mvdr), 1e-9 (oracle_reverb)   */
   int max_batch;     /* utterances per call                                          */
   int max_samples;   /* longest utterance (samples)                                  */
+  int beamformer;    /* AVZ_BF_*                                                     */
+  double bypass_hz;  /* AVZ_BF_HYBRID_NULL: bins with f < bypass_hz pass mic 0 (200)  */
+  double cond_max;   /* AVZ_BF_HYBRID_NULL: delay-and-sum above this 2-norm condition
+                        number of [v_tgt, v_int] (10, inference.py:80)               */
 } avz_config;
 
 typedef struct avz_plan avz_plan;
@@ -109,6 +120,25 @@ int avz_stft(const avz_plan* plan, int batch, int channels, const int* len, int 
              const float* x, long long x_stride, long long ch_stride, float* Y,
              long long y_stride_b, long long y_stride_c, long long y_stride_f,
              void* hip_stream);
+
+/* Final_pipeline driver chunking (Final_pipeline/src/inference.py:171-188): copy
+ * item i = samples [item_start[i], item_start[i] + chunk) of utterance item_utt[i]
+ * (zero beyond len[utt], the driver's np.pad of the tail chunk) for each of
+ * `channels` planar channels into items[i][c][0..chunk). Device arrays. */
+int avz_chunk_split(int n_items, int channels, int chunk, const int* item_utt,
+                    const int* item_start, const int* len, const float* x, long long x_stride,
+                    long long x_ch_stride, float* items, long long item_stride,
+                    long long item_ch_stride, void* hip_stream);
+
+/* Final_pipeline driver overlap-add (inference.py:224-236): for utterance b with
+ * chunks c = 0 .. ceil(len[b]/hop) - 1 stored as items item_base[b] + c, each adding
+ * item_out[...][0 .. min(item_out_len, len[b] - c hop)) at sample c hop:
+ * y[b][n] = (sum of the covering chunk outputs) / max(count, 1); peak[b] = max|y[b]|;
+ * with normalize != 0, y[b] /= peak[b] + norm_eps (1e-9 in the reference). */
+int avz_chunk_merge(int batch, int max_len, int hop, int item_out_len, const int* len,
+                    const int* item_base, const float* item_out, long long item_out_stride,
+                    float* y, long long y_stride, float* peak, int normalize, double norm_eps,
+                    void* hip_stream);
 
 const char* avz_strerror(int code);
 /* Last HIP error string recorded by the library on this thread (diagnostics). */

@@ -314,6 +314,140 @@ def external_mask_vec(y_mix, mask_target, n_fft=1024, hop=512, sigma=1e-5, d=0.0
 
 
 # ----------------------------------------------------------------------------
+# Final_pipeline: hybrid hard-null beamformer + 2-s chunked overlap-add driver
+# ----------------------------------------------------------------------------
+D_FINAL = 0.08          # Final_pipeline/src/config.py:29 (MIC_DIST)
+WIN_SIZE = 32000        # Final_pipeline/src/config.py:17 (chunk), hop = WIN_SIZE // 2
+BYPASS_HZ = 200.0       # Final_pipeline/src/inference.py:50
+COND_MAX = 10.0         # Final_pipeline/src/inference.py:80
+
+
+def steering_vector_phase_norm(f: float, angle_deg: float = ANGLE_TARGET, d: float = D_FINAL,
+                               c: float = C_SOUND) -> np.ndarray:
+    """Final_pipeline/src/inference.py:16-26: far-field vector divided by (v[0] + 1e-10)."""
+    th = np.deg2rad(angle_deg)
+    om = 2 * np.pi * f
+    v = np.array([[np.exp(-1j * om * ((d / 2) * np.cos(th) / c))],
+                  [np.exp(-1j * om * ((d / 2) * np.cos(th - np.pi) / c))]])
+    return v / (v[0] + 1e-10)
+
+
+def hybrid_weights_loop(Y: np.ndarray, mask: np.ndarray, f_bins: np.ndarray,
+                        d: float = D_FINAL, bypass_hz: float = BYPASS_HZ,
+                        cond_max: float = COND_MAX) -> np.ndarray:
+    """Per-bin weights of Final_pipeline/src/inference.py:28-98 (hybrid_hard_null_bf),
+    loop-faithful: complex64 noise covariance (:57-60), LAPACK eigh principal vector
+    phase-normalised to mic 0 (:63-67), cond of [v_tgt, v_int] (:77), delay-and-sum
+    fallback or solve C^H w = [1, 0] (:79-91). Returns W [F, 2] complex128; the bypass
+    bins (f < bypass_hz, :50-52) get w = [1, 0] (S = Y0)."""
+    F = Y.shape[1]
+    m_int = 1.0 - mask
+    W = np.zeros((F, 2), dtype=np.complex128)
+    e1 = np.array([[1], [0]], dtype=np.complex64)
+    for k in range(F):
+        fk = f_bins[k]
+        if fk < bypass_hz:
+            W[k] = [1.0, 0.0]
+            continue
+        Yk = Y[:, k, :]
+        mk = m_int[k, :]
+        R = (Yk * mk) @ Yk.conj().T / (np.sum(mk) + 1e-6)
+        _, vecs = np.linalg.eigh(R)
+        v_int = vecs[:, -1].reshape(2, 1)
+        v_int = v_int / (v_int[0] / (np.abs(v_int[0]) + 1e-10))
+        v_tgt = steering_vector_phase_norm(fk, ANGLE_TARGET, d, C_SOUND)
+        C = np.column_stack((v_tgt, v_int))
+        if np.linalg.cond(C) > cond_max:
+            w = v_tgt / 2
+        else:
+            try:
+                w = np.linalg.solve(C.conj().T, e1)
+            except np.linalg.LinAlgError:
+                w = v_tgt / 2
+        W[k] = w[:, 0]
+    return W
+
+
+def hybrid_weights_vec(Y: np.ndarray, mask: np.ndarray, f_bins: np.ndarray,
+                       d: float = D_FINAL, bypass_hz: float = BYPASS_HZ,
+                       cond_max: float = COND_MAX) -> np.ndarray:
+    """Closed-form fp64 form of hybrid_weights_loop (the engine's per-bin algebra):
+    principal eigenvector of the 2x2 Hermitian R, cond_2 = sigma_max^2 / |det C|,
+    w = [conj v1, -conj v0] / conj(det C). A bin whose eigenvector has v[0] == 0 (where
+    the reference divides by zero) takes the delay-and-sum fallback."""
+    Yd = Y.astype(np.complex128)
+    m = (1.0 - mask).astype(np.float64)
+    nrm = m.sum(axis=1) + 1e-6
+    a = np.einsum("ft,ft->f", m, np.abs(Yd[0]) ** 2) / nrm
+    e = np.einsum("ft,ft->f", m, np.abs(Yd[1]) ** 2) / nrm
+    b = np.einsum("ft,ft->f", m, Yd[0] * Yd[1].conj()) / nrm
+    lam = 0.5 * (a + e) + np.sqrt((0.5 * (a - e)) ** 2 + np.abs(b) ** 2)
+    u0 = np.where(a >= e, lam - e + 0j, b)
+    u1 = np.where(a >= e, b.conj(), lam - a + 0j)
+    un = np.sqrt(np.abs(u0) ** 2 + np.abs(u1) ** 2)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        u0, u1 = u0 / un, u1 / un
+        a0 = np.abs(u0)
+        v0 = a0 + 1e-10 + 0j
+        v1 = u1 * u0.conj() * (a0 + 1e-10) / a0 ** 2
+    vt = np.stack([steering_vector_phase_norm(fk, ANGLE_TARGET, d, C_SOUND)[:, 0]
+                   for fk in f_bins])
+    t0, t1 = vt[:, 0], vt[:, 1]
+    det = t0 * v1 - v0 * t1
+    p = np.abs(t0) ** 2 + np.abs(t1) ** 2
+    q = np.abs(v0) ** 2 + np.abs(v1) ** 2
+    r = t0.conj() * v0 + t1.conj() * v1
+    smax2 = 0.5 * (p + q) + np.sqrt((0.5 * (p - q)) ** 2 + np.abs(r) ** 2)
+    ok = np.isfinite(v1) & (a0 > 0) & (np.abs(det) > 0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ok &= smax2 <= cond_max * np.abs(det)
+        W = np.where(ok[:, None], np.stack([v1.conj(), -v0.conj()], axis=1) / det.conj()[:, None],
+                     vt / 2)
+    W[f_bins < bypass_hz] = [1.0, 0.0]
+    return W
+
+
+def enhance_chunked(y: np.ndarray, mask_fn, bf="loop", n_fft: int = 1024, chunk: int = WIN_SIZE,
+                    fs: int = FS, d: float = D_FINAL):
+    """Final_pipeline/src/inference.py:160-237 (enhance_audio minus file I/O): y [S, 2]
+    float32; ``mask_fn(c, start, chunk_samples [chunk, 2]) -> M [F, T]`` target probability
+    (stands in for TFLiteBeamformer.predict_mask). Chunks of ``chunk`` samples every
+    chunk // 2 with a zero-padded tail (:179-188), hybrid weights, x M post-filter (:219),
+    iSTFT, time-domain overlap-add / count (:226-229), peak normalisation + 1e-9 (:236)."""
+    hop_c = chunk // 2
+    L = len(y)
+    out = np.zeros(L)
+    cnt = np.zeros(L)
+    wfn = hybrid_weights_loop if bf == "loop" else hybrid_weights_vec
+    for c in range(int(np.ceil(L / hop_c))):
+        start = c * hop_c
+        seg = y[start:start + chunk]
+        if len(seg) < chunk:
+            seg = np.pad(seg, ((0, chunk - len(seg)), (0, 0)))
+        f, _, Y = stft(seg.T, fs=fs, nperseg=n_fft, noverlap=n_fft // 2)
+        M = mask_fn(c, start, seg)
+        W = wfn(Y, M, f, d=d)
+        S = np.einsum("fm,mft->ft", W.conj(), Y) * M
+        _, xo = istft(S, fs=fs, nperseg=n_fft, noverlap=n_fft // 2)
+        n = min(len(xo), L - start)
+        out[start:start + n] += xo[:n]
+        cnt[start:start + n] += 1.0
+    final = out / np.maximum(cnt, 1.0)
+    return final / (np.max(np.abs(final)) + 1e-9)
+
+
+def chunk_target_mask(tgt: np.ndarray, itf: np.ndarray, start: int, chunk: int = WIN_SIZE,
+                      n_fft: int = 1024) -> np.ndarray:
+    """Oracle target mask |S_t| >= |S_i| of one driver chunk (the stand-in for the absent
+    TFLite mask model used by the golden fixtures, tests/golden/make_golden.py)."""
+    st = np.pad(tgt[start:start + chunk], (0, max(0, chunk - len(tgt[start:start + chunk]))))
+    si = np.pad(itf[start:start + chunk], (0, max(0, chunk - len(itf[start:start + chunk]))))
+    _, _, St = stft(st, nperseg=n_fft, noverlap=n_fft // 2)
+    _, _, Si = stft(si, nperseg=n_fft, noverlap=n_fft // 2)
+    return (np.abs(St) >= np.abs(Si)).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------
 # metrics
 # ----------------------------------------------------------------------------
 def projection_sdr_sir(output, target, interf):

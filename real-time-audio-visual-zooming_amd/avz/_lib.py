@@ -27,10 +27,12 @@ AVZ_ERR_ALIGN = -5
 MASK_IBM, MASK_IPD, MASK_EXTERNAL = 0, 1, 2
 PF_NONE, PF_IBM_TARGET, PF_EXT_FLOOR, PF_EXT_MUL = 0, 1, 2, 3
 NORM_NONE, NORM_PEAK = 0, 1
+BF_MVDR, BF_HYBRID_NULL = 0, 1
 
 EXPORTED = [
     "avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
-    "avz_mvdr_batch", "avz_stft", "avz_strerror", "avz_last_hip_error", "avz_version",
+    "avz_mvdr_batch", "avz_stft", "avz_chunk_split", "avz_chunk_merge", "avz_strerror",
+    "avz_last_hip_error", "avz_version",
 ]
 
 
@@ -43,6 +45,7 @@ class AvzConfig(ct.Structure):
         ("pf_floor", ct.c_double), ("weight_eps", ct.c_double),
         ("normalize", ct.c_int), ("norm_eps", ct.c_double),
         ("max_batch", ct.c_int), ("max_samples", ct.c_int),
+        ("beamformer", ct.c_int), ("bypass_hz", ct.c_double), ("cond_max", ct.c_double),
     ]
 
 
@@ -91,11 +94,15 @@ def _load():
     lib.avz_mvdr_batch.argtypes = [P, ct.POINTER(AvzBatchArgs), P]
     lib.avz_stft.argtypes = [P, ct.c_int, ct.c_int, P, ct.c_int, P, ct.c_longlong, ct.c_longlong,
                              P, ct.c_longlong, ct.c_longlong, ct.c_longlong, P]
+    I, LL = ct.c_int, ct.c_longlong
+    lib.avz_chunk_split.argtypes = [I, I, I, P, P, P, P, LL, LL, P, LL, LL, P]
+    lib.avz_chunk_merge.argtypes = [I, I, I, I, P, P, P, LL, P, LL, P, I, ct.c_double, P]
     lib.avz_strerror.argtypes = [ct.c_int]
     lib.avz_strerror.restype = ct.c_char_p
     lib.avz_last_hip_error.restype = ct.c_char_p
     for name in ("avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
-                 "avz_mvdr_batch", "avz_stft", "avz_version"):
+                 "avz_mvdr_batch", "avz_stft", "avz_chunk_split", "avz_chunk_merge",
+                 "avz_version"):
         getattr(lib, name).restype = ct.c_int
     return lib
 

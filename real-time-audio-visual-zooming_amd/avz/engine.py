@@ -4,7 +4,7 @@
 (rt_av_zoom/core/oracle_debug.py:42-94, rt_av_zoom/core/masked_mvdr.py:76-128,
 rt_av_zoom/core/full_audio_generating_pipeline/inference.py:88-118): one call runs
 STFT -> mask -> masked covariance -> MVDR -> apply/post-filter -> iSTFT (-> peak
-normalisation) for a whole batch of utterances in a single kernel launch.
+normalisation) for a whole batch of utterances in one chain of kernel launches (analysis, solve, synthesis, finalize).
 """
 from __future__ import annotations
 
@@ -20,6 +20,7 @@ MASKS = {"ibm": _lib.MASK_IBM, "ipd": _lib.MASK_IPD, "external": _lib.MASK_EXTER
 POSTFILTERS = {"none": _lib.PF_NONE, "ibm": _lib.PF_IBM_TARGET, "floor": _lib.PF_EXT_FLOOR,
                "mul": _lib.PF_EXT_MUL}
 NORMS = {"none": _lib.NORM_NONE, "peak": _lib.NORM_PEAK}
+BEAMFORMERS = {"mvdr": _lib.BF_MVDR, "hybrid_null": _lib.BF_HYBRID_NULL}
 
 
 def n_frames(length: int, hop: int) -> int:
@@ -49,6 +50,9 @@ class PlanConfig:
     norm_eps: float = 0.0
     max_batch: int = 1
     max_samples: int = 64000
+    beamformer: str = "mvdr"
+    bypass_hz: float = 200.0
+    cond_max: float = 10.0
     extra: dict = field(default_factory=dict)
 
 
@@ -80,6 +84,8 @@ class MVDRPlan:
         c.pf_floor, c.weight_eps = cfg.pf_floor, cfg.weight_eps
         c.normalize, c.norm_eps = NORMS[cfg.normalize], cfg.norm_eps
         c.max_batch, c.max_samples = cfg.max_batch, cfg.max_samples
+        c.beamformer = BEAMFORMERS[cfg.beamformer]
+        c.bypass_hz, c.cond_max = cfg.bypass_hz, cfg.cond_max
         h = ct.c_void_p()
         check(lib.avz_plan_create(ct.byref(h), ct.byref(c)), "avz_plan_create")
         self._h = h

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <complex>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -15,9 +16,7 @@ struct avz_plan {
   avz_config cfg;
   double tau1, tau2;         // far-field delays of the two mics (masked_mvdr.py:28-29)
   int max_frames;
-  uint8_t* maskbits;         // [max_batch][ceil(max_frames/4)][F] IBM nibbles (fused path)
-  long long mb_stride;
-  // chunked path workspace, one allocation (see avz_internal.h FusedArgs)
+  // chunked path workspace, one allocation (see avz_internal.h ChainArgs)
   int nchunk;
   void* arena;
   float* part;
@@ -27,7 +26,6 @@ struct avz_plan {
   float* heads;
   float* tails;
   uint32_t* peak_u;
-  bool use_fused;            // AVZ_KERNEL_PATH=fused selects the one-block-per-utterance kernel
 };
 
 static thread_local std::string g_last_hip;
@@ -71,6 +69,8 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
       c.mask_mode != AVZ_MASK_EXTERNAL)
     return AVZ_ERR_ARG;
   if (c.normalize != AVZ_NORM_NONE && c.normalize != AVZ_NORM_PEAK) return AVZ_ERR_ARG;
+  if (c.beamformer != AVZ_BF_MVDR && c.beamformer != AVZ_BF_HYBRID_NULL) return AVZ_ERR_ARG;
+  if (c.beamformer == AVZ_BF_HYBRID_NULL && !(c.cond_max >= 1.0)) return AVZ_ERR_ARG;
 
   avz_plan* p = new (std::nothrow) avz_plan();
   if (!p) return AVZ_ERR_ARG;
@@ -81,15 +81,6 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
   p->tau2 = (c.mic_d / 2) * std::cos(0.0) * std::cos(theta - M_PI) / c.c_sound;
   p->max_frames = frames_for(c.max_samples, c.hop);
   const int F = c.n_fft / 2 + 1;
-  p->mb_stride = (long long)((p->max_frames + 3) / 4 + 1) * F;
-  p->maskbits = nullptr;
-  if (c.mask_mode == AVZ_MASK_IBM) {
-    hipError_t e = hipMalloc((void**)&p->maskbits, (size_t)p->mb_stride * c.max_batch);
-    if (e != hipSuccess) {
-      delete p;
-      return hip_fail(e);
-    }
-  }
   {
     const int H = c.n_fft / 2;
     const long long B = c.max_batch;
@@ -103,7 +94,6 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
     const size_t sz_b = up(sizeof(uint32_t) * B);
     hipError_t e = hipMalloc(&p->arena, sz_part + sz_mw + sz_steer + sz_coef + 2 * sz_ht + sz_b);
     if (e != hipSuccess) {
-      if (p->maskbits) (void)hipFree(p->maskbits);
       delete p;
       return hip_fail(e);
     }
@@ -116,25 +106,31 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
     p->tails = reinterpret_cast<float*>(q); q += sz_ht;
     p->peak_u = reinterpret_cast<uint32_t*>(q);
     // d_m(f_k) = exp(-1j * (2 pi f_k) * tau_m), f_k = np.fft.rfftfreq(n_fft, 1/fs)[k]
+    // (masked_mvdr.py:22-35); the hybrid null beamformer phase-normalises it to mic 0,
+    // v / (v[0] + 1e-10) (Final_pipeline/src/inference.py:16-26).
     std::vector<double> st((size_t)F * 4);
     const double df = 1.0 / (c.n_fft * (1.0 / c.fs));
     for (int k = 0; k < F; ++k) {
       const double omega = 2 * M_PI * (k * df);
-      const double x1 = -omega * p->tau1, x2 = -omega * p->tau2;
-      st[4 * k + 0] = std::cos(x1);
-      st[4 * k + 1] = std::sin(x1);
-      st[4 * k + 2] = std::cos(x2);
-      st[4 * k + 3] = std::sin(x2);
+      const std::complex<double> v0 = std::exp(std::complex<double>(0.0, -omega * p->tau1));
+      const std::complex<double> v1 = std::exp(std::complex<double>(0.0, -omega * p->tau2));
+      std::complex<double> d0 = v0, d1 = v1;
+      if (c.beamformer == AVZ_BF_HYBRID_NULL) {
+        const std::complex<double> den = v0 + 1e-10;
+        d0 = v0 / den;
+        d1 = v1 / den;
+      }
+      st[4 * k + 0] = d0.real();
+      st[4 * k + 1] = d0.imag();
+      st[4 * k + 2] = d1.real();
+      st[4 * k + 3] = d1.imag();
     }
     e = hipMemcpy(p->steer, st.data(), sizeof(double) * st.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       (void)hipFree(p->arena);
-      if (p->maskbits) (void)hipFree(p->maskbits);
       delete p;
       return hip_fail(e);
     }
-    const char* path = std::getenv("AVZ_KERNEL_PATH");
-    p->use_fused = path && std::strcmp(path, "fused") == 0;
   }
   *out = p;
   return AVZ_OK;
@@ -142,7 +138,6 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
 
 extern "C" int avz_plan_destroy(avz_plan* p) {
   if (!p) return AVZ_ERR_ARG;
-  if (p->maskbits) (void)hipFree(p->maskbits);
   if (p->arena) (void)hipFree(p->arena);
   delete p;
   return AVZ_OK;
@@ -178,7 +173,7 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   }
   if (c.mask_mode == AVZ_MASK_EXTERNAL && !a->ext_mask) return AVZ_ERR_ARG;
 
-  avz::FusedArgs k{};
+  avz::ChainArgs k{};
   k.batch = a->batch;
   k.len = a->len;
   k.mix = a->mix;
@@ -196,8 +191,6 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   k.peak = a->peak;
   k.cov_out = a->cov_out;
   k.w_out = a->w_out;
-  k.maskbits = p->maskbits;
-  k.mb_stride = p->mb_stride;
   k.fs = c.fs;
   k.sigma = c.sigma;
   k.tau1 = p->tau1;
@@ -217,8 +210,10 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   k.heads = p->heads;
   k.tails = p->tails;
   k.peak_u = p->peak_u;
-  const int rc = p->use_fused ? avz_launch_fused(c.n_fft, c.mask_mode, &k, stream)
-                              : avz_launch_chunked(c.n_fft, c.mask_mode, &k, stream);
+  k.beamformer = c.beamformer;
+  k.bypass_hz = c.bypass_hz;
+  k.cond_max = c.cond_max;
+  const int rc = avz_launch_chunked(c.n_fft, c.mask_mode, &k, stream);
   if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
   return rc;
 }
@@ -247,6 +242,60 @@ extern "C" int avz_stft(const avz_plan* p, int batch, int channels, const int* l
   s.y_stride_f = y_stride_f;
   s.max_frames = T;
   const int rc = avz_launch_stft(p->cfg.n_fft, &s, stream);
+  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  return rc;
+}
+
+extern "C" int avz_chunk_split(int n_items, int channels, int chunk, const int* item_utt,
+                               const int* item_start, const int* len, const float* x,
+                               long long x_stride, long long x_ch_stride, float* items,
+                               long long item_stride, long long item_ch_stride, void* stream) {
+  if (n_items < 0 || chunk <= 0 || (channels != 1 && channels != 2)) return AVZ_ERR_SHAPE;
+  if (n_items == 0) return AVZ_OK;
+  if (!item_utt || !item_start || !len || !x || !items) return AVZ_ERR_ARG;
+  if (item_ch_stride < chunk && channels > 1) return AVZ_ERR_SHAPE;
+  if (n_items > 1 && item_stride < (long long)channels * chunk) return AVZ_ERR_SHAPE;
+  avz::ChunkSplitArgs s{};
+  s.n_items = n_items;
+  s.channels = channels;
+  s.chunk = chunk;
+  s.item_utt = item_utt;
+  s.item_start = item_start;
+  s.len = len;
+  s.x = x;
+  s.x_stride = x_stride;
+  s.x_ch_stride = x_ch_stride;
+  s.items = items;
+  s.item_stride = item_stride;
+  s.item_ch_stride = item_ch_stride;
+  const int rc = avz_launch_chunk_split(&s, stream);
+  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  return rc;
+}
+
+extern "C" int avz_chunk_merge(int batch, int max_len, int hop, int item_out_len, const int* len,
+                               const int* item_base, const float* item_out,
+                               long long item_out_stride, float* y, long long y_stride,
+                               float* peak, int normalize, double norm_eps, void* stream) {
+  if (batch < 0 || max_len < 0 || hop <= 0 || item_out_len <= 0) return AVZ_ERR_SHAPE;
+  if (batch == 0 || max_len == 0) return AVZ_OK;
+  if (!len || !item_base || !item_out || !y || !peak) return AVZ_ERR_ARG;
+  if (item_out_stride < item_out_len || (batch > 1 && y_stride < max_len)) return AVZ_ERR_SHAPE;
+  avz::ChunkMergeArgs m{};
+  m.batch = batch;
+  m.max_len = max_len;
+  m.hop = hop;
+  m.item_out_len = item_out_len;
+  m.len = len;
+  m.item_base = item_base;
+  m.item_out = item_out;
+  m.item_out_stride = item_out_stride;
+  m.y = y;
+  m.y_stride = y_stride;
+  m.peak = peak;
+  m.normalize = normalize != 0;
+  m.norm_eps = (float)norm_eps;
+  const int rc = avz_launch_chunk_merge(&m, stream);
   if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
   return rc;
 }

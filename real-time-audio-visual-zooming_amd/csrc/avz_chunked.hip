@@ -90,7 +90,7 @@ __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<
 
 // Mask value m and covariance weight of one (bin, frame).
 template <int MASK>
-__device__ __forceinline__ float bin_mask(const FusedArgs& A, int b, cf x0, cf x1, cf zr,
+__device__ __forceinline__ float bin_mask(const ChainArgs& A, int b, cf x0, cf x1, cf zr,
                                           cf zrp, int k, int t, bool& noise, float& wgt) {
   if constexpr (MASK == MASK_IBM) {
     // 2T = zr + conj(zrp), 2I = (zr - conj zrp)/i ; |2I|^2 > |2T|^2 <=> |I| > |T|
@@ -113,7 +113,7 @@ __device__ __forceinline__ float bin_mask(const FusedArgs& A, int b, cf x0, cf x
 
 // ================================ analysis ================================
 template <int N, int MASK>
-__global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(FusedArgs A) {
+__global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A) {
   using C = KCfg<N>;
   using G = CGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
@@ -272,12 +272,13 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(FusedArgs A)
 }
 
 // ================================ solve ================================
-// One thread per (utterance, bin): sum the chunk partials in fp64, closed-form MVDR
-// with the plan's steering table -> coef[b][k] (+ optional cov/w debug outputs).
+// One thread per (utterance, bin): sum the chunk partials in fp64, closed-form MVDR or
+// hybrid hard-null weights with the plan's steering table -> coef[b][k] (+ optional
+// cov/w debug outputs).
 constexpr int kSolveThreads = 256;
 
 template <int N>
-__global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(FusedArgs A) {
+__global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   constexpr int H = N / 2, F = N / 2 + 1;
   const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
   if (idx >= (long long)A.batch * F) return;
@@ -294,8 +295,11 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(FusedArgs A) {
   }
   const double* d = A.steer + 4 * k;
   cf al, be;
-  mvdr_solve_d(R, k, N, A, d[0], d[1], d[2], d[3], al, be,
-               A.w_out ? A.w_out + ((long long)b * F + k) * 4 : nullptr);
+  float* wdbg = A.w_out ? A.w_out + ((long long)b * F + k) * 4 : nullptr;
+  if (A.beamformer == BF_HYBRID_NULL)
+    hybrid_solve_d(R, k, N, A, d[0], d[1], d[2], d[3], al, be, wdbg);
+  else
+    mvdr_solve_d(R, k, N, A, d[0], d[1], d[2], d[3], al, be, wdbg);
   reinterpret_cast<float4*>(A.coef)[(long long)b * F + k] = make_float4(al.x, al.y, be.x, be.y);
   if (A.cov_out) {
 #pragma unroll
@@ -305,7 +309,7 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(FusedArgs A) {
 
 // ================================ synthesis ================================
 template <int N, int PF>
-__global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(FusedArgs A) {
+__global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(ChainArgs A) {
   using C = KCfg<N>;
   using G = CGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
@@ -541,7 +545,7 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(FusedArgs A
 
 // ================================ finalize ================================
 template <int N>
-__global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(FusedArgs A) {
+__global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
   constexpr int NT = kCThreads, H = N / 2, NWAVE = NT / 64;
   __shared__ float red[NWAVE];
   const int c = blockIdx.x, b = blockIdx.y;
@@ -607,7 +611,7 @@ static bool set_lds(K kern, int lds) {
 }
 
 template <int N, int MASK, int PF>
-static int launch_chunked_t(const FusedArgs* a, hipStream_t st) {
+static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   auto k1 = avz_analysis_kernel<N, MASK>;
   auto k2 = avz_synthesis_kernel<N, PF>;
   auto k3 = avz_finalize_kernel<N>;
@@ -631,7 +635,7 @@ static int launch_chunked_t(const FusedArgs* a, hipStream_t st) {
 }
 
 template <int N, int MASK>
-static int launch_pf(const FusedArgs* a, hipStream_t st) {
+static int launch_pf(const ChainArgs* a, hipStream_t st) {
   if constexpr (MASK == MASK_IBM) {
     if (a->postfilter == PF_IBM_TARGET) return launch_chunked_t<N, MASK, PF_IBM_TARGET>(a, st);
   }
@@ -643,7 +647,7 @@ static int launch_pf(const FusedArgs* a, hipStream_t st) {
   return -4;
 }
 
-extern "C" int avz_launch_chunked(int n_fft, int mask_mode, const FusedArgs* a, void* stream) {
+extern "C" int avz_launch_chunked(int n_fft, int mask_mode, const ChainArgs* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (a->batch <= 0) return 0;
   if (n_fft == 1024) {

@@ -8,9 +8,6 @@
 
 namespace avz {
 
-constexpr int kThreads = 1024;
-constexpr int kWaves = 16;
-
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 __device__ __forceinline__ rsrc_t make_rsrc(const float* p, long long n_floats) {
@@ -79,7 +76,7 @@ struct KCfg<512> {
   static constexpr int TW_BYTES = 0;
 };
 
-template <int N, int NT = kThreads>
+template <int N, int NT>
 struct Geo {
   using C = KCfg<N>;
   static constexpr int NWAVE = NT / 64;
@@ -173,13 +170,28 @@ struct Acc64 {
   }
 };
 
+// Apply coefficients of weights w: S = conj(w0) y0 + conj(w1) y1 evaluated on the packed
+// mic pair Z = y0 + i y1 as S = alpha Z[k] + beta conj(Z[N-k]).
+__device__ __forceinline__ void coef_from_w(double w0r, double w0i, double w1r, double w1i,
+                                            cf& alpha, cf& beta, float* w_dbg) {
+  // alpha = (conj w0 - i conj w1)/2 ; beta = (conj w0 + i conj w1)/2
+  alpha = {(float)(0.5 * (w0r - w1i)), (float)(0.5 * (-w0i - w1r))};
+  beta = {(float)(0.5 * (w0r + w1i)), (float)(0.5 * (-w0i + w1r))};
+  if (w_dbg) {
+    w_dbg[0] = (float)w0r;
+    w_dbg[1] = (float)w0i;
+    w_dbg[2] = (float)w1r;
+    w_dbg[3] = (float)w1i;
+  }
+}
+
 // Per-bin MVDR solve in fp64 (oracle_debug.py:66-79):
 //   w~ = (R/(sum m + 1e-6) + sigma I)^{-1} d ; w = w~ / (d^H w~ + 1e-10);
 //   singular -> w = [1, 0]; f < fmin -> w = 0.
-// d = steering vector (masked_mvdr.py:22-35). Returns the apply coefficients
-// S = alpha Z[k] + beta conj(Z[N-k]) of the packed mic pair.
+// d = steering vector (masked_mvdr.py:22-35). c = {sum m|y0|^2, sum m|y1|^2,
+// Re/Im sum m y0 conj(y1), sum m}.
 __device__ __forceinline__ void mvdr_solve_d(const double (&c)[5], int k, int n_fft,
-                                             const FusedArgs& A, double d0r, double d0i,
+                                             const ChainArgs& A, double d0r, double d0i,
                                              double d1r, double d1i, cf& alpha, cf& beta,
                                              float* w_dbg) {
   double w0r = 0, w0i = 0, w1r = 0, w1i = 0;
@@ -208,26 +220,74 @@ __device__ __forceinline__ void mvdr_solve_d(const double (&c)[5], int k, int n_
       w1i = (t1i * dr - t1r * di) / dd;
     }
   }
-  // alpha = (conj w0 - i conj w1)/2 ; beta = (conj w0 + i conj w1)/2
-  alpha = {(float)(0.5 * (w0r - w1i)), (float)(0.5 * (-w0i - w1r))};
-  beta = {(float)(0.5 * (w0r + w1i)), (float)(0.5 * (-w0i + w1r))};
-  if (w_dbg) {
-    w_dbg[0] = (float)w0r;
-    w_dbg[1] = (float)w0i;
-    w_dbg[2] = (float)w1r;
-    w_dbg[3] = (float)w1i;
-  }
+  coef_from_w(w0r, w0i, w1r, w1i, alpha, beta, w_dbg);
 }
 
-// Same, steering vector d_m = exp(-i 2 pi f_k tau_m) evaluated here in fp64.
-__device__ __forceinline__ void mvdr_solve(const double (&c)[5], int k, int n_fft,
-                                           const FusedArgs& A, cf& alpha, cf& beta,
-                                           float* w_dbg) {
-  const double om = 2.0 * M_PI * ((double)k * A.fs / (double)n_fft);
-  double s1, c1, s2, c2;
-  sincos(om * A.tau1, &s1, &c1);
-  sincos(om * A.tau2, &s2, &c2);
-  mvdr_solve_d(c, k, n_fft, A, c1, -s1, c2, -s2, alpha, beta, w_dbg);
+// Per-bin hybrid hard-null weights in fp64 (Final_pipeline/src/inference.py:28-98):
+//   f < bypass_hz -> w = [1, 0] (mic 0 passes);
+//   R = sum m y y^H / (sum m + 1e-6), v_int = principal eigenvector of R with v_int[0]
+//   made real: v_int * (|v_int[0]| + 1e-10) / v_int[0];
+//   C = [v_tgt, v_int]; cond_2(C) > cond_max (or singular) -> w = v_tgt / 2,
+//   else w = (C^H)^-1 [1, 0]^T.
+// v_tgt = (vt0, vt1): the plan's phase-normalised steering vector (inference.py:16-26).
+// Where the reference's eigenvector has v_int[0] == 0 (R diagonal with R11 >= R00, e.g.
+// no noise-weighted frames) it divides by zero and np.linalg.cond then raises; here
+// that bin takes the delay-and-sum fallback.
+__device__ __forceinline__ void hybrid_solve_d(const double (&c)[5], int k, int n_fft,
+                                               const ChainArgs& A, double t0r, double t0i,
+                                               double t1r, double t1i, cf& alpha, cf& beta,
+                                               float* w_dbg) {
+  const double fk = (double)k * A.fs / (double)n_fft;
+  if (fk < A.bypass_hz) {
+    coef_from_w(1.0, 0.0, 0.0, 0.0, alpha, beta, w_dbg);
+    return;
+  }
+  const double nrm = c[4] + 1e-6;
+  const double a = c[0] / nrm, e = c[1] / nrm;
+  const double br = c[2] / nrm, bi = c[3] / nrm;  // R01 = b, R10 = conj(b)
+  const double b2 = br * br + bi * bi;
+  const double hd = 0.5 * (a - e);
+  const double lam = 0.5 * (a + e) + sqrt(hd * hd + b2);
+  // eigenvector of lam: [lam - e, conj b] (a >= e) or [b, lam - a] (a < e)
+  double u0r, u0i, u1r, u1i;
+  if (a >= e) {
+    u0r = lam - e; u0i = 0.0; u1r = br; u1i = -bi;
+  } else {
+    u0r = br; u0i = bi; u1r = lam - a; u1i = 0.0;
+  }
+  const double un = sqrt(u0r * u0r + u0i * u0i + u1r * u1r + u1i * u1i);
+  u0r /= un; u0i /= un; u1r /= un; u1i /= un;
+  // v = u (|u0| + 1e-10) / u0 = u conj(u0) (|u0| + 1e-10) / |u0|^2
+  const double m0 = u0r * u0r + u0i * u0i;
+  const double a0 = sqrt(m0);
+  const double g = (a0 + 1e-10) / m0;
+  const double v0r = a0 + 1e-10, v0i = 0.0;
+  const double v1r = (u1r * u0r + u1i * u0i) * g;
+  const double v1i = (u1i * u0r - u1r * u0i) * g;
+  double w0r = 0.5 * t0r, w0i = 0.5 * t0i, w1r = 0.5 * t1r, w1i = 0.5 * t1i;  // delay-and-sum
+  if (isfinite(v1r) && isfinite(v1i) && m0 > 0.0) {
+    // det C = t0 v1 - v0 t1
+    const double dr = (t0r * v1r - t0i * v1i) - (v0r * t1r - v0i * t1i);
+    const double di = (t0r * v1i + t0i * v1r) - (v0r * t1i + v0i * t1r);
+    const double det2 = dr * dr + di * di;
+    // sigma_max^2 of C: eigenvalue of C^H C = [[p, r], [conj r, q]]
+    const double p = t0r * t0r + t0i * t0i + t1r * t1r + t1i * t1i;
+    const double q = v0r * v0r + v0i * v0i + v1r * v1r + v1i * v1i;
+    const double rr = t0r * v0r + t0i * v0i + t1r * v1r + t1i * v1i;  // conj(t) . v
+    const double ri = t0r * v0i - t0i * v0r + t1r * v1i - t1i * v1r;
+    const double hpq = 0.5 * (p - q);
+    const double smax2 = 0.5 * (p + q) + sqrt(hpq * hpq + rr * rr + ri * ri);
+    // cond = smax2 / |det C|; keep the solve only when cond <= cond_max
+    if (det2 > 0.0 && smax2 <= A.cond_max * sqrt(det2)) {
+      // w = [conj(v1), -conj(v0)] / conj(det C)
+      const double ir = dr / det2, ii = di / det2;  // 1 / conj(det) = det / |det|^2
+      w0r = v1r * ir + v1i * ii;
+      w0i = v1r * ii - v1i * ir;
+      w1r = -(v0r * ir + v0i * ii);
+      w1i = -(v0r * ii - v0i * ir);
+    }
+  }
+  coef_from_w(w0r, w0i, w1r, w1i, alpha, beta, w_dbg);
 }
 
 __device__ __forceinline__ cf apply_bin(cf alpha, cf beta, cf z, cf zp, float g) {

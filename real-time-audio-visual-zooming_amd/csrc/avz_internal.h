@@ -8,8 +8,10 @@ enum : int { MASK_IBM = 0, MASK_IPD = 1, MASK_EXTERNAL = 2 };
 enum : int { PF_NONE = 0, PF_IBM_TARGET = 1, PF_EXT_FLOOR = 2, PF_EXT_MUL = 3 };
 enum : int { NORM_NONE = 0, NORM_PEAK = 1 };
 
-// Everything the fused kernel needs, passed by value.
-struct FusedArgs {
+enum : int { BF_MVDR = 0, BF_HYBRID_NULL = 1 };
+
+// Everything the analysis / solve / synthesis / finalize chain needs, passed by value.
+struct ChainArgs {
   int batch;
   const int* len;             // [B] samples per utterance (device)
   const float* mix;           // [B][2][..] planar
@@ -25,11 +27,11 @@ struct FusedArgs {
   float* peak;                // [B] or null: max|out| before normalisation
   double* cov_out;            // [B][F][5] or null: sum m|y0|^2, sum m|y1|^2, Re/Im sum m y0 y1*, sum m
   float* w_out;               // [B][F][4] or null: Re w0, Im w0, Re w1, Im w1
-  uint8_t* maskbits;          // workspace, [B][ceil(T/4)][F] nibbles (IBM post-filter)
-  long long mb_stride;        // bytes between utterances
   double fs, sigma, tau1, tau2, fmin_hz;
   float weight_eps, pf_floor, norm_eps;
   int postfilter, normalize;
+  int beamformer;             // BF_*
+  double bypass_hz, cond_max; // hybrid null: mic-0 bypass below, delay-and-sum above
   // chunked path workspace (plan-owned)
   int max_frames;             // frames of the longest utterance (grid extent)
   int nchunk;                 // allocated 32-frame chunks per utterance (workspace stride)
@@ -52,12 +54,36 @@ struct StftArgs {
   int max_frames;
 };
 
+struct ChunkSplitArgs {
+  int n_items, channels, chunk;
+  const int* item_utt;        // [n_items] source utterance
+  const int* item_start;      // [n_items] first sample
+  const int* len;             // [B] utterance lengths
+  const float* x;             // [B][channels][..]
+  long long x_stride, x_ch_stride;
+  float* items;               // [n_items][channels][..]
+  long long item_stride, item_ch_stride;
+};
+
+struct ChunkMergeArgs {
+  int batch, max_len, hop, item_out_len;
+  const int* len;             // [B]
+  const int* item_base;       // [B] index of each utterance's first item
+  const float* item_out;      // [n_items][item_out_stride]
+  long long item_out_stride;
+  float* y;                   // [B][y_stride]
+  long long y_stride;
+  float* peak;                // [B] max |y| before normalisation
+  int normalize;
+  float norm_eps;
+};
+
 }  // namespace avz
 
 extern "C" {
-int avz_launch_fused(int n_fft, int mask_mode, const avz::FusedArgs* a, void* stream);
-int avz_launch_chunked(int n_fft, int mask_mode, const avz::FusedArgs* a, void* stream);
+int avz_launch_chunk_split(const avz::ChunkSplitArgs* a, void* stream);
+int avz_launch_chunk_merge(const avz::ChunkMergeArgs* a, void* stream);
+int avz_launch_chunked(int n_fft, int mask_mode, const avz::ChainArgs* a, void* stream);
 int avz_chunk_frames(void);
 int avz_launch_stft(int n_fft, const avz::StftArgs* a, void* stream);
-int avz_fused_lds_bytes(int n_fft);
 }

@@ -15,7 +15,11 @@ How the reference is run:
 * Intermediates are captured by wrapping scipy.signal.stft/istft and
   numpy.linalg.solve for the duration of one reference call.
 
-Usage:  python tests/golden/make_golden.py      (writes tests/golden/*.npz)
+Final_pipeline/src/inference.py imports tensorflow at module level; an empty stand-in
+module is injected (only TFLiteBeamformer uses it, and that class is replaced by
+_MaskFeeder below because the .tflite model file is absent).
+
+Usage:  python tests/golden/make_golden.py [hybrid]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -168,10 +172,105 @@ def stage_dict(rec, n_fft):
     return out
 
 
+# ----------------------------------------------------------------------------- Final_pipeline
+class _MaskFeeder:
+    """Stand-in for Final_pipeline's TFLiteBeamformer: the .tflite model is absent
+    (.MISSING_LARGE_BLOBS:1) and TensorFlow is not installed, so predict_mask returns
+    the oracle TARGET mask of the chunk, |S_t| >= |S_i| (SURVEY 8(c) hybrid row), and
+    records the features the reference computed for it."""
+    masks: list = []
+    features: list = []
+
+    def __init__(self, model_path):
+        self.i = 0
+
+    def predict_mask(self, log_mag, raw_ipd):
+        _MaskFeeder.features.append((np.array(log_mag), np.array(raw_ipd)))
+        m = _MaskFeeder.masks[self.i]
+        self.i += 1
+        return m
+
+
+def install_final_pipeline():
+    tf = types.ModuleType("tensorflow")
+    tf.lite = types.SimpleNamespace(Interpreter=None)
+    sys.modules.setdefault("tensorflow", tf)
+    from src import config, inference  # Final_pipeline/src (on sys.path via install_reference)
+    return inference, config
+
+
+def chunk_target_masks(tgt, itf, n_total, chunk=32000, hop=16000, n_fft=1024):
+    """Per-chunk oracle target masks with the driver's chunking (inference.py:171-181)."""
+    masks = []
+    for c in range(int(np.ceil(n_total / hop))):
+        seg_t = tgt[c * hop:c * hop + chunk]
+        seg_i = itf[c * hop:c * hop + chunk]
+        seg_t = np.pad(seg_t, (0, chunk - len(seg_t)))
+        seg_i = np.pad(seg_i, (0, chunk - len(seg_i)))
+        _, _, St = scipy.signal.stft(seg_t, fs=16000, nperseg=n_fft, noverlap=n_fft - n_fft // 2)
+        _, _, Si = scipy.signal.stft(seg_i, fs=16000, nperseg=n_fft, noverlap=n_fft - n_fft // 2)
+        masks.append((np.abs(St) >= np.abs(Si)).astype(np.float32))
+    return masks
+
+
+def run_enhance_audio(inference, config, mix16, tgt, itf):
+    """Run Final_pipeline enhance_audio (inference.py:144-237) on a stereo int16 mixture
+    with the oracle target masks; returns (final output, first hybrid call's I/O)."""
+    calls = []
+    orig_bf = inference.hybrid_hard_null_bf
+
+    def bf(Y, mask, f_bins):
+        S = orig_bf(Y, mask, f_bins)
+        if not calls:
+            calls.append((np.array(Y), np.array(mask), np.array(f_bins), np.array(S)))
+        return S
+
+    _MaskFeeder.masks = chunk_target_masks(tgt, itf, len(mix16))
+    _MaskFeeder.features = []
+    with tempfile.TemporaryDirectory() as td:
+        inp = os.path.join(td, "mixture.wav")
+        wavfile.write(inp, 16000, mix16)
+        old = (config.RESULTS_DIR, inference.TFLiteBeamformer, inference.hybrid_hard_null_bf)
+        config.RESULTS_DIR = td
+        inference.TFLiteBeamformer = _MaskFeeder
+        inference.hybrid_hard_null_bf = bf
+        _WRITES.clear()
+        try:
+            with contextlib.redirect_stdout(open(os.devnull, "w")):
+                inference.enhance_audio("golden", inp, os.path.join(td, "absent.tflite"))
+        finally:
+            config.RESULTS_DIR, inference.TFLiteBeamformer, inference.hybrid_hard_null_bf = old
+    return _WRITES["golden_enhanced.wav"], calls[0], list(_MaskFeeder.features)
+
+
+def gen_final_pipeline(trip, run_metrics, save):
+    inference, config = install_final_pipeline()
+    for k, (m, t, i) in trip.items():
+        tf = t.astype(np.float32) / 32768.0
+        itf = i.astype(np.float32) / 32768.0
+        out, (Y, mask, fb, S), feats = run_enhance_audio(inference, config, m, tf, itf)
+        L = min(len(out), len(tf))
+        sdr_o, sir_o = run_metrics.calculate_metrics_manual(out[:L], tf[:L], itf[:L])
+        arrays = dict(chunk=config.WIN_SIZE, hop=config.WIN_SIZE // 2, n_fft=config.N_FFT,
+                      mic_d=config.MIC_DIST, c=config.C_SPEED, out=out.astype(np.float32),
+                      sumsq=np.sum(out ** 2), sir_out=sir_o, sdr_out=sdr_o,
+                      n_chunks=len(_MaskFeeder.masks))
+        if k == "test":
+            arrays.update(chunk0_Y=Y.astype(np.complex64), chunk0_mask=mask, chunk0_f=fb,
+                          chunk0_S=S.astype(np.complex64),
+                          chunk0_logmag=feats[0][0].astype(np.float32),
+                          chunk0_ipd=feats[0][1].astype(np.float32))
+        save(f"hybrid_{k}.npz", **arrays)
+
+
 def main():
     od, mm, run_metrics, metrics = install_reference()
+    mpath = os.path.join(HERE, "MANIFEST.json")
     manifest = {"generator": "tests/golden/make_golden.py", "reference": REF,
                 "scipy": scipy.__version__, "numpy": np.__version__, "files": {}}
+    only = sys.argv[1:]  # e.g. "hybrid": regenerate one family, keep the rest
+    if only and os.path.exists(mpath):
+        manifest["files"] = json.load(open(mpath))["files"]
 
     def save(name, **arrays):
         path = os.path.join(HERE, name)
@@ -179,8 +278,15 @@ def main():
         manifest["files"][name] = sorted(arrays)
         print("wrote", name, os.path.getsize(path) // 1024, "KiB")
 
-    # -- bundled inputs (data files of the reference, int16) --------------------
     trip = {k: load_triple(k) for k in TRIPLES}
+    if only:
+        if "hybrid" in only:
+            gen_final_pipeline(trip, run_metrics, save)
+        with open(mpath, "w") as fh:
+            json.dump(manifest, fh, indent=1, sort_keys=True)
+        return
+
+    # -- bundled inputs (data files of the reference, int16) --------------------
     for k, (m, t, i) in trip.items():
         save(f"inputs_{k}.npz", mix=m, tgt=t, int=i)
 
@@ -256,6 +362,9 @@ def main():
     sv = np.stack([mm.get_steering_vector(a, fk, d, 343.0)[:, 0]
                    for a, d in ((90.0, 0.01), (40.0, 0.08), (130.0, 0.04)) for fk in f])
     save("steering.npz", f=f, sv=sv.reshape(3, len(f), 2))
+
+    # -- Final_pipeline hybrid hard-null driver (run.py inf / batch_run) -----------
+    gen_final_pipeline(trip, run_metrics, save)
 
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)
