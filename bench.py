@@ -1,11 +1,13 @@
-"""Headline benchmark: beamformed TF-bins/s of the fused MVDR hot path on MI355X.
+"""Headline benchmark: beamformed TF-bins/s of the MVDR hot path on MI355X.
 
 Workload (BASELINE.json configs[1]): per GPU a batch of B = 256 synthetic 2-mic
 utterances of 4.0 s (64000 samples @ 16 kHz), 2 interferers, oracle IBM mask,
 1024-pt STFT / hop 512 -> F x T = 513 x 126 = 64,638 TF-bins per utterance.
-One step = one launch of the fused kernel over the whole batch (STFT -> IBM ->
-masked covariance -> fp64 MVDR solve -> apply + IBM post-filter -> iSTFT -> peak
-normalisation), inputs resident in HBM. Multi-GPU: one process per GPU, utterances
+One step = one avz_mvdr_batch call over the whole batch: the analysis (STFT -> IBM ->
+masked covariance partials), solve (fp64 MVDR), synthesis (STFT -> apply + IBM
+post-filter -> iSTFT/OLA) and finalize (chunk seams, peak normalisation) kernels,
+inputs resident in HBM. Per-kernel times come from HIP events the plan records
+around each launch on the launch stream (avz_plan_set_timing). Multi-GPU: one process per GPU, utterances
 sharded (weak scaling, no data-path collective); the only collective is the final
 RCCL all-reduce of the SIR metric sums (and the max-over-ranks step time).
 
@@ -44,6 +46,8 @@ def parse():
                     help="time box of the CPU baseline workers")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, available cores)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="skip the per-kernel HIP events (roofline from the step events)")
     return ap.parse_args()
 
 
@@ -138,6 +142,8 @@ def main():
     torch.cuda.synchronize()
 
     K = args.steps
+    if not args.no_kernel_timing:
+        plan.set_timing(True)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(K)]
     if world > 1:
@@ -153,7 +159,8 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    chain_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kt = plan.timing() if not args.no_kernel_timing else None
 
     # ---- final metrics: projection SIR per utterance (run_metrics.py:6-36), RCCL all-reduce
     n_out = plan.out_len(S)
@@ -177,9 +184,12 @@ def main():
     if world > 1:
         dist.all_reduce(sums)
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        kt = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
-        kern_ms = float(kt.item())
+        mx = torch.tensor([chain_ms] + ([kt[k] for k in plan.KERNELS] if kt else []),
+                          dtype=torch.float64, device=dev)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        chain_ms = float(mx[0])
+        if kt:
+            kt.update({k: float(mx[1 + j]) for j, k in enumerate(plan.KERNELS)})
     # SIR delta vs the reference restatement on identical inputs (rank 0, few utterances)
     d_sir = None
     if rank == 0:
@@ -195,14 +205,38 @@ def main():
     F, T = N_FFT // 2 + 1, -(-S // HOP) + 1
     bins_per_rank = B * F * T
     value = world * bins_per_rank * K / t_max
-    alg_bytes = B * (4 * S * 4 + n_out * 4)  # 2 mic + 2 ref streams in, 1 out (fp32)
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    # Algorithmic bytes: the analysis kernel reads the 2 mic + 2 reference
+    # streams (4 x 4 B per sample = 15.97 B per TF-bin); the whole chain adds the output
+    # stream (19.96 B per TF-bin).
+    alg_analysis = B * 4 * S * 4
+    alg_chain = B * (4 * S * 4 + n_out * 4)
+    traffic = {}
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         pm = json.load(open(tf))
         if pm.get("batch") == B and pm.get("n_fft") == N_FFT and pm.get("samples") == S:
-            traffic = pm.get("hbm_bytes_per_launch")
+            traffic = pm.get("hbm_bytes_per_launch", {})
+            if not isinstance(traffic, dict):
+                traffic = {}
+    if kt:
+        dom_ms = kt["analysis"]
+        roof = {"bound": "hbm", "achieved": alg_analysis / (dom_ms * 1e-3) / 1e9,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": alg_analysis / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "traffic": traffic.get("analysis"),
+                "kernel": "avz_analysis_kernel<1024,IBM>", "kernel_ms": dom_ms,
+                "alg_bytes_per_launch": alg_analysis,
+                "kernels_ms": {k: kt[k] for k in plan.KERNELS},
+                "chain": {"achieved": alg_chain / (chain_ms * 1e-3) / 1e9, "ms": chain_ms,
+                          "alg_bytes_per_launch": alg_chain,
+                          "frac": alg_chain / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                          "traffic": traffic.get("chain")}}
+    else:
+        roof = {"bound": "hbm", "achieved": alg_chain / (chain_ms * 1e-3) / 1e9,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": alg_chain / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "traffic": traffic.get("chain"), "kernel": "avz_mvdr_batch chain",
+                "kernel_ms": chain_ms, "alg_bytes_per_launch": alg_chain}
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "TF-bins/s", "n_gpus": world,
@@ -215,10 +249,7 @@ def main():
                        "n_fft": N_FFT, "hop": HOP, "tf_bins_per_utt": F * T, "sigma": 1.0,
                        "mask": "ibm", "postfilter": "ibm", "normalize": "peak",
                        "parallelism": f"utterance-sharded x{world}, RCCL metric all-reduce only"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "avz_fused_kernel<1024,IBM>", "kernel_ms": kern_ms,
-                         "alg_bytes_per_launch": alg_bytes},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "sir": {"sir_in_mean_db": float(sums[0] / sums[2]),
                     "sir_out_mean_db": float(sums[1] / sums[2]),

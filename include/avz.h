@@ -112,6 +112,13 @@ int avz_plan_get_config(const avz_plan* plan, avz_config* cfg);
 int avz_num_frames(const avz_plan* plan, int len);
 int avz_mvdr_batch(const avz_plan* plan, const avz_batch_args* args, void* hip_stream);
 
+/* Diagnostics: record HIP events around the four kernels of every avz_mvdr_batch call
+ * on this plan (analysis, solve, synthesis, finalize; enable != 0 also resets the
+ * sums). avz_plan_get_timing waits for the outstanding calls and returns the average
+ * milliseconds per kernel over the calls recorded since enabling. Not thread-safe. */
+int avz_plan_set_timing(avz_plan* plan, int enable);
+int avz_plan_get_timing(avz_plan* plan, double* ms_avg /*[4]*/, int* calls);
+
 /* Stage API: STFT of [batch][channels][x_stride] real signals into complex64
  * Y[b][c][k][t] (interleaved re/im floats) with element strides; replaces the
  * reference's scipy.signal.stft(x, fs, nperseg=n_fft, noverlap=n_fft/2) calls

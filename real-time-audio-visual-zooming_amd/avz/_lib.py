@@ -31,7 +31,8 @@ BF_MVDR, BF_HYBRID_NULL = 0, 1
 
 EXPORTED = [
     "avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
-    "avz_mvdr_batch", "avz_stft", "avz_chunk_split", "avz_chunk_merge", "avz_strerror",
+    "avz_mvdr_batch", "avz_plan_set_timing", "avz_plan_get_timing", "avz_stft",
+    "avz_chunk_split", "avz_chunk_merge", "avz_strerror",
     "avz_last_hip_error", "avz_version",
 ]
 
@@ -95,6 +96,8 @@ def _load():
     lib.avz_stft.argtypes = [P, ct.c_int, ct.c_int, P, ct.c_int, P, ct.c_longlong, ct.c_longlong,
                              P, ct.c_longlong, ct.c_longlong, ct.c_longlong, P]
     I, LL = ct.c_int, ct.c_longlong
+    lib.avz_plan_set_timing.argtypes = [P, I]
+    lib.avz_plan_get_timing.argtypes = [P, ct.POINTER(ct.c_double), ct.POINTER(I)]
     lib.avz_chunk_split.argtypes = [I, I, I, P, P, P, P, LL, LL, P, LL, LL, P]
     lib.avz_chunk_merge.argtypes = [I, I, I, I, P, P, P, LL, P, LL, P, I, ct.c_double, P]
     lib.avz_strerror.argtypes = [ct.c_int]
@@ -102,6 +105,7 @@ def _load():
     lib.avz_last_hip_error.restype = ct.c_char_p
     for name in ("avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
                  "avz_mvdr_batch", "avz_stft", "avz_chunk_split", "avz_chunk_merge",
+                 "avz_plan_set_timing", "avz_plan_get_timing",
                  "avz_version"):
         getattr(lib, name).restype = ct.c_int
     return lib

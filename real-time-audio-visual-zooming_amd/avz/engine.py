@@ -98,6 +98,20 @@ class MVDRPlan:
             lib.avz_plan_destroy(h)
             self._h = None
 
+    # ------------------------------------------------------------------ diagnostics
+    KERNELS = ("analysis", "solve", "synthesis", "finalize")
+
+    def set_timing(self, enable: bool = True) -> None:
+        """Record HIP events around each of the chain's four kernels on every run()."""
+        check(lib.avz_plan_set_timing(self._h, int(enable)), "avz_plan_set_timing")
+
+    def timing(self) -> dict:
+        """Average ms per kernel over the runs since set_timing(True) (waits for them)."""
+        ms = (ct.c_double * 4)()
+        n = ct.c_int()
+        check(lib.avz_plan_get_timing(self._h, ms, ct.byref(n)), "avz_plan_get_timing")
+        return {"calls": n.value, **{k: ms[i] for i, k in enumerate(self.KERNELS)}}
+
     # ------------------------------------------------------------------ helpers
     def frames(self, length: int) -> int:
         return check(lib.avz_num_frames(self._h, int(length)), "avz_num_frames")

@@ -26,7 +26,32 @@ struct avz_plan {
   float* heads;
   float* tails;
   uint32_t* peak_u;
+  // diagnostic per-kernel timing (avz_plan_set_timing): two event sets used alternately
+  bool timing;
+  hipEvent_t ev[2][5];
+  bool ev_pending[2];
+  int ev_next;
+  double ms_sum[4];
+  int ms_calls;
 };
+
+static void timing_drain(avz_plan* p, int set) {
+  if (!p->ev_pending[set]) return;
+  p->ev_pending[set] = false;
+  if (hipEventSynchronize(p->ev[set][4]) != hipSuccess) return;
+  for (int i = 0; i < 4; ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p->ev[set][i], p->ev[set][i + 1]) == hipSuccess) p->ms_sum[i] += ms;
+  }
+  p->ms_calls += 1;
+}
+
+static void timing_free(avz_plan* p) {
+  if (!p->timing) return;
+  for (int s = 0; s < 2; ++s)
+    for (int i = 0; i < 5; ++i) (void)hipEventDestroy(p->ev[s][i]);
+  p->timing = false;
+}
 
 static thread_local std::string g_last_hip;
 
@@ -138,6 +163,7 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
 
 extern "C" int avz_plan_destroy(avz_plan* p) {
   if (!p) return AVZ_ERR_ARG;
+  timing_free(p);
   if (p->arena) (void)hipFree(p->arena);
   delete p;
   return AVZ_OK;
@@ -210,12 +236,54 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   k.heads = p->heads;
   k.tails = p->tails;
   k.peak_u = p->peak_u;
+  avz_plan* mp = const_cast<avz_plan*>(p);  // timing state only (diagnostic)
+  void* evs[5];
+  int set = -1;
+  if (mp->timing) {
+    set = mp->ev_next;
+    mp->ev_next ^= 1;
+    timing_drain(mp, set);  // the call two back: the previous call keeps the GPU busy
+    for (int i = 0; i < 5; ++i) evs[i] = mp->ev[set][i];
+    k.events = evs;
+  }
   k.beamformer = c.beamformer;
   k.bypass_hz = c.bypass_hz;
   k.cond_max = c.cond_max;
   const int rc = avz_launch_chunked(c.n_fft, c.mask_mode, &k, stream);
   if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  if (set >= 0 && rc == AVZ_OK) mp->ev_pending[set] = true;
   return rc;
+}
+
+extern "C" int avz_plan_set_timing(avz_plan* p, int enable) {
+  if (!p) return AVZ_ERR_ARG;
+  timing_free(p);
+  p->ev_pending[0] = p->ev_pending[1] = false;
+  p->ev_next = 0;
+  p->ms_calls = 0;
+  for (double& m : p->ms_sum) m = 0.0;
+  if (!enable) return AVZ_OK;
+  for (int s = 0; s < 2; ++s)
+    for (int i = 0; i < 5; ++i) {
+      const hipError_t e = hipEventCreateWithFlags(&p->ev[s][i], hipEventDisableSystemFence);
+      if (e != hipSuccess) {
+        for (int t = 0; t <= s; ++t)
+          for (int j = 0; j < (t < s ? 5 : i); ++j) (void)hipEventDestroy(p->ev[t][j]);
+        return hip_fail(e);
+      }
+    }
+  p->timing = true;
+  return AVZ_OK;
+}
+
+extern "C" int avz_plan_get_timing(avz_plan* p, double* ms_avg, int* calls) {
+  if (!p || !ms_avg) return AVZ_ERR_ARG;
+  if (!p->timing) return AVZ_ERR_ARG;
+  timing_drain(p, p->ev_next);
+  timing_drain(p, p->ev_next ^ 1);
+  for (int i = 0; i < 4; ++i) ms_avg[i] = p->ms_calls ? p->ms_sum[i] / p->ms_calls : 0.0;
+  if (calls) *calls = p->ms_calls;
+  return AVZ_OK;
 }
 
 extern "C" int avz_stft(const avz_plan* p, int batch, int channels, const int* len, int max_len,

@@ -627,10 +627,19 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   const dim3 grid(nch, a->batch);
   constexpr int F = N / 2 + 1;
   const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
+  hipEvent_t const* ev = reinterpret_cast<hipEvent_t const*>(a->events);
+  auto mark = [&](int i) {
+    if (ev) (void)hipEventRecord(ev[i], st);
+  };
+  mark(0);
   hipLaunchKernelGGL(k1, grid, dim3(kCThreads), lds, st, *a);
+  mark(1);
   hipLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, *a);
+  mark(2);
   hipLaunchKernelGGL(k2, grid, dim3(kCThreads), lds, st, *a);
+  mark(3);
   hipLaunchKernelGGL(k3, grid, dim3(kCThreads), 0, st, *a);
+  mark(4);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -42,6 +42,7 @@ struct ChainArgs {
   float* heads;               // [B][nchunk][H] chunk's first frame, first-half contribution
   float* tails;               // [B][nchunk][H] chunk's last frame, second-half contribution
   uint32_t* peak_u;           // [B] max |out| over chunk interiors (float bits, atomicMax)
+  void* const* events;        // host-only: 5 hipEvent_t recorded around the 4 launches, or null
 };
 
 struct StftArgs {

@@ -1,15 +1,16 @@
 """Turn rocprofv3 PMC CSVs (separate FETCH_SIZE and WRITE_SIZE passes) into per-launch
-HBM traffic of the fused kernel -> profiles/pmc_traffic.json (read by bench.py).
+HBM traffic of each kernel of the MVDR chain -> profiles/pmc_traffic.json (read by
+bench.py for roofline.traffic).
 
-Correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950
-FETCH_SIZE reports half the bytes of wide coalesced reads (128-B requests tallied at
-64 B). Our loads are 4 B/lane buffer_load_dword (a width the guide lists as
-uncalibrated); calibration against the design's known byte count: with x2 the read
-side equals algorithmic reads + the pass-2 mix re-read + the normalisation re-read
-(262 + 131 + 65 = 458 MB at B = 256) to <1 %, so `hbm_bytes_per_launch` uses
-2 x FETCH_SIZE + WRITE_SIZE.
+Correction (MI355X_MICROARCH.md section HBM): FETCH_SIZE / WRITE_SIZE are in KiB; on
+gfx950 FETCH_SIZE under-counts wide reads (128-B requests tallied at 64 B). Our reads are
+4-B-per-lane buffer_load_dword streams, a width the guide leaves uncalibrated; round r01
+calibrated x2 on a kernel whose read bytes were known by construction (profiles/r01), and
+that factor is applied here. `analysis_read_check` = 2 x FETCH_SIZE of the analysis kernel
+over its compulsory input bytes (2 mic + 2 reference streams) shows how tight it is.
+Writes are taken as reported.
 
-  python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv>
+  python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv>
 """
 import csv
 import json
@@ -17,35 +18,40 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = {"analysis": "avz_analysis_kernel", "solve": "avz_solve_kernel",
+           "synthesis": "avz_synthesis_kernel", "finalize": "avz_finalize_kernel"}
+B, S, N = 256, 64000, 1024
 
 
 def per_dispatch(path, counter):
-    vals = {}
+    vals = {k: {} for k in KERNELS}
     with open(path) as fh:
         for row in csv.DictReader(fh):
-            if "avz_fused_kernel" not in row.get("Kernel_Name", ""):
-                continue
             if row.get("Counter_Name") != counter:
                 continue
-            d = int(row["Dispatch_Id"])
-            vals[d] = vals.get(d, 0.0) + float(row["Counter_Value"])
-    return list(vals.values())
+            name = row.get("Kernel_Name", "")
+            for k, pat in KERNELS.items():
+                if pat in name:
+                    d = int(row["Dispatch_Id"])
+                    vals[k][d] = vals[k].get(d, 0.0) + float(row["Counter_Value"])
+    return {k: (sum(v.values()) / len(v) if v else None) for k, v in vals.items()}
 
 
 def main():
     fetch = per_dispatch(sys.argv[1], "FETCH_SIZE")
     write = per_dispatch(sys.argv[2], "WRITE_SIZE")
-    f_kib = sum(fetch) / len(fetch)
-    w_kib = sum(write) / len(write)
-    B, S, N = 256, 64000, 1024
-    alg = B * (4 * S * 4 + S * 4)
-    out = {"kernel": "avz_fused_kernel<1024,IBM,512>", "batch": B, "samples": S, "n_fft": N,
-           "dispatches": [len(fetch), len(write)],
-           "fetch_kib_per_launch": f_kib, "write_kib_per_launch": w_kib,
-           "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024,
-           "hbm_bytes_per_launch_raw": (f_kib + w_kib) * 1024,
-           "alg_bytes_per_launch": alg,
-           "read_correction": "2 x FETCH_SIZE (gfx950 half-count; calibrated vs known bytes)"}
+    alg_reads = B * 4 * S * 4
+    factor = 2.0
+    hbm = {k: (factor * fetch[k] + write[k]) * 1024 for k in KERNELS}
+    hbm["chain"] = sum(hbm.values())
+    n_out = (-(-S // (N // 2))) * (N // 2)
+    out = {"kernels": KERNELS, "batch": B, "samples": S, "n_fft": N,
+           "fetch_kib_per_launch": fetch, "write_kib_per_launch": write,
+           "read_factor": factor, "hbm_bytes_per_launch": hbm,
+           "analysis_read_check": factor * fetch["analysis"] * 1024 / alg_reads,
+           "alg_bytes_per_launch": {"analysis": alg_reads, "chain": alg_reads + B * n_out * 4},
+           "note": "reads = 2 x FETCH_SIZE (gfx950 half-count, calibrated in profiles/r01); "
+                   "writes = WRITE_SIZE"}
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1))
