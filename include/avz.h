@@ -147,6 +147,21 @@ int avz_chunk_merge(int batch, int max_len, int hop, int item_out_len, const int
                     float* y, long long y_stride, float* peak, int normalize, double norm_eps,
                     void* hip_stream);
 
+/* Mask-model input features straight from the time-domain mic pair (device arrays):
+ *  AVZ_FEAT_LOGMAG_IPD: feat[b*s_b + c*s_c + k*s_f + t*s_t], c = 0: log(|Y0| + 1e-7),
+ *    c = 1: angle(Y0) - angle(Y1) — the U-Net input of
+ *    full_audio_generating_pipeline/inference.py:90-94 (NCHW with s_t = 1);
+ *  AVZ_FEAT_TFLITE: c = 0..3: log_mag, sin(ipd), cos(ipd), linspace(0, 1, F)[k] — the
+ *    TFLite input of Final_pipeline/src/inference.py:198-203, 117-128 (NHWC: s_c = 1,
+ *    s_t = 4, s_f = 4 T).
+ * Y = scipy.signal.stft(x, nperseg=n_fft, noverlap=n_fft/2) of the plan's n_fft. */
+#define AVZ_FEAT_LOGMAG_IPD 1
+#define AVZ_FEAT_TFLITE 2
+int avz_mask_features(const avz_plan* plan, int layout, int batch, const int* len, int max_len,
+                      const float* x, long long x_stride, long long ch_stride, float* feat,
+                      long long s_b, long long s_c, long long s_f, long long s_t,
+                      void* hip_stream);
+
 const char* avz_strerror(int code);
 /* Last HIP error string recorded by the library on this thread (diagnostics). */
 const char* avz_last_hip_error(void);

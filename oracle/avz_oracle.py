@@ -436,6 +436,22 @@ def enhance_chunked(y: np.ndarray, mask_fn, bf="loop", n_fft: int = 1024, chunk:
     return final / (np.max(np.abs(final)) + 1e-9)
 
 
+def mask_features(y2: np.ndarray, n_fft: int = 1024, layout: str = "unet") -> np.ndarray:
+    """Mask-model inputs of a [2, S] mic pair, float32 as numpy computes them:
+    "unet"   -> [2, F, T]  log(|Y0| + 1e-7), angle(Y0) - angle(Y1)
+                (full_audio_generating_pipeline/inference.py:90-94);
+    "tflite" -> [F, T, 4]  + sin/cos of the IPD and linspace(0, 1, F)
+                (Final_pipeline/src/inference.py:198-203, 117-128)."""
+    _, _, Y = stft(y2, nperseg=n_fft, noverlap=n_fft // 2)
+    lm = np.log(np.abs(Y[0]) + 1e-7)
+    ipd = np.angle(Y[0]) - np.angle(Y[1])
+    if layout == "unet":
+        return np.stack([lm, ipd])
+    F, T = lm.shape
+    fm = np.tile(np.linspace(0, 1, F, dtype=np.float32)[:, None], (1, T))
+    return np.stack([lm, np.sin(ipd), np.cos(ipd), fm], axis=-1)
+
+
 def chunk_target_mask(tgt: np.ndarray, itf: np.ndarray, start: int, chunk: int = WIN_SIZE,
                       n_fft: int = 1024) -> np.ndarray:
     """Oracle target mask |S_t| >= |S_i| of one driver chunk (the stand-in for the absent

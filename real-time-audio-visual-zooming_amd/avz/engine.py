@@ -199,3 +199,40 @@ class MVDRPlan:
                            ct.c_void_p(Y.data_ptr()), Y.stride(0), Y.stride(1), Y.stride(2),
                            _stream_handle(stream)), "avz_stft")
         return Y
+
+
+FEATURE_LAYOUTS = {"unet": _lib.FEAT_LOGMAG_IPD, "tflite": _lib.FEAT_TFLITE}
+
+
+def mask_features(plan: MVDRPlan, x: torch.Tensor, layout: str = "unet", lengths=None,
+                  max_len=None, stream=None) -> torch.Tensor:
+    """Mask-model input features of a [B, 2, S] mic pair (avz_mask_features):
+    layout "unet"   -> [B, 2, F, T]: log(|Y0| + 1e-7), angle(Y0) - angle(Y1)
+                       (full_audio_generating_pipeline/inference.py:90-94);
+    layout "tflite" -> [B, F, T, 4]: log_mag, sin(ipd), cos(ipd), linspace(0, 1, F)
+                       (Final_pipeline/src/inference.py:198-203, 117-128)."""
+    if x.dim() != 3 or x.shape[1] != 2 or x.dtype != torch.float32 or x.stride(2) != 1 \
+            or not x.is_cuda:
+        raise ValueError("x must be float32 [B, 2, S] on the device")
+    B, _, S = x.shape
+    if lengths is None:
+        lengths = torch.full((B,), S, dtype=torch.int32, device=x.device)
+        max_len = S
+    if max_len is None:
+        max_len = int(lengths.max().item())
+    T = n_frames(max_len, plan.hop)
+    F = plan.F
+    if layout == "unet":
+        out = torch.zeros((B, 2, F, T), dtype=torch.float32, device=x.device)
+        sb, sc, sf, st = out.stride()
+    elif layout == "tflite":
+        out = torch.zeros((B, F, T, 4), dtype=torch.float32, device=x.device)
+        sb, sf, st, sc = out.stride()
+    else:
+        raise ValueError(f"unknown feature layout {layout!r}")
+    check(lib.avz_mask_features(plan._h, FEATURE_LAYOUTS[layout], B,
+                                ct.c_void_p(lengths.data_ptr()), int(max_len),
+                                ct.c_void_p(x.data_ptr()), x.stride(0), x.stride(1),
+                                ct.c_void_p(out.data_ptr()), sb, sc, sf, st,
+                                _stream_handle(stream)), "avz_mask_features")
+    return out

@@ -367,3 +367,32 @@ extern "C" int avz_chunk_merge(int batch, int max_len, int hop, int item_out_len
   if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
   return rc;
 }
+
+extern "C" int avz_mask_features(const avz_plan* p, int layout, int batch, const int* len,
+                                 int max_len, const float* x, long long x_stride,
+                                 long long ch_stride, float* feat, long long s_b, long long s_c,
+                                 long long s_f, long long s_t, void* stream) {
+  if (!p || !len || !x || !feat) return AVZ_ERR_ARG;
+  if (layout != AVZ_FEAT_LOGMAG_IPD && layout != AVZ_FEAT_TFLITE) return AVZ_ERR_ARG;
+  if (batch < 0) return AVZ_ERR_SHAPE;
+  if (batch == 0) return AVZ_OK;
+  if (max_len < p->cfg.n_fft || max_len > p->cfg.max_samples) return AVZ_ERR_SHAPE;
+  if (ch_stride < max_len) return AVZ_ERR_SHAPE;
+  avz::StftArgs s{};
+  s.batch = batch;
+  s.channels = 2;
+  s.len = len;
+  s.x = x;
+  s.x_stride = x_stride;
+  s.ch_stride = ch_stride;
+  s.max_frames = frames_for(max_len, p->cfg.hop);
+  s.feat = layout;
+  s.F_out = feat;
+  s.f_sb = s_b;
+  s.f_sc = s_c;
+  s.f_sf = s_f;
+  s.f_st = s_t;
+  const int rc = avz_launch_stft(p->cfg.n_fft, &s, stream);
+  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  return rc;
+}

@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "avz_common.hpp"
 
 namespace avz {
@@ -162,10 +164,17 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A)
   cf v[PPL];
   auto issue_loads = [&](int step) {
     const int s0 = (t0 + step * FB + my_frame) * H - N / 2 + lm.in0;
-    static_for<0, PPL>([&](auto r) {
-      v[r].x = bload(r_re, s0 + C::IN_STRIDE * r);
-      v[r].y = bload(r_im, s0 + C::IN_STRIDE * r);
-    });
+    if (t0 + step * FB + wave_frame0 >= 1) {  // wave-uniform: no negative sample index
+      static_for<0, PPL>([&](auto r) {
+        v[r].x = bload_nn(r_re, s0 + C::IN_STRIDE * r);
+        v[r].y = bload_nn(r_im, s0 + C::IN_STRIDE * r);
+      });
+    } else {
+      static_for<0, PPL>([&](auto r) {
+        v[r].x = bload(r_re, s0 + C::IN_STRIDE * r);
+        v[r].y = bload(r_im, s0 + C::IN_STRIDE * r);
+      });
+    }
   };
 
   Acc32 acc[BPT];
@@ -197,35 +206,57 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A)
     lds_barrier();
     AVZ_STAMP(1);
     const int nvalid = min(FB, T - f0);
+    // Thread-per-bin over the step's frames. A full step runs unguarded so all of its
+    // LDS reads can issue back to back; only a chunk's last step may be partial.
+    auto bin_phase = [&](auto full) {
+      // frames whose reads are batched together (IPD: one, its inlined atan2f fallback is big)
+      constexpr int G = (MASK == MASK_IPD) ? 1 : (FB < 4 ? FB : 4);
 #pragma unroll
-    for (int j = 0; j < BPT; ++j) {
-      const int kb = tid + j * NT;
-      const int kp = (N - kb) & (N - 1);
+      for (int j = 0; j < BPT; ++j) {
+        const int kb = tid + j * NT;
+        const int kp = (N - kb) & (N - 1);
 #pragma unroll
-      for (int i = 0; i < FB; ++i) {
-        if (i < nvalid) {
-          const cf* Zm = slot_ptr<N>(lds, i);
-          cf x0, x1, zr{0, 0}, zrp{0, 0};
-          split_pair(Zm[kb], Zm[kp], x0, x1);
-          if constexpr (MASK == MASK_IBM) {
-            const cf* Zr = slot_ptr<N>(lds, FB + i);
-            zr = Zr[kb];
-            zrp = Zr[kp];
+        for (int g0 = 0; g0 < FB; g0 += G) {
+          cf zm[G], zmp[G], zr[G], zrp[G];
+#pragma unroll
+          for (int i = 0; i < G; ++i) {
+            if (decltype(full)::value || g0 + i < nvalid) {
+              const cf* Zm = slot_ptr<N>(lds, g0 + i);
+              zm[i] = Zm[kb];
+              zmp[i] = Zm[kp];
+              if constexpr (MASK == MASK_IBM) {
+                const cf* Zr = slot_ptr<N>(lds, FB + g0 + i);
+                zr[i] = Zr[kb];
+                zrp[i] = Zr[kp];
+              }
+            }
           }
-          bool noise = false;
-          float wgt;
-          const float m = bin_mask<MASK>(A, b, x0, x1, zr, zrp, kb, f0 + i, noise, wgt);
-          bits[j] |= (noise ? 1u : 0u) << (step * FB + i);
-          acc[j].add(x0, x1, wgt, m);
+#pragma unroll
+          for (int i = 0; i < G; ++i) {
+            if (decltype(full)::value || g0 + i < nvalid) {
+              cf x0, x1;
+              split_pair2(zm[i], zmp[i], x0, x1);  // 2 y0, 2 y1
+              bool noise = false;
+              float wgt;
+              const float m =
+                  bin_mask<MASK>(A, b, x0, x1, zr[i], zrp[i], kb, f0 + g0 + i, noise, wgt);
+              bits[j] |= (noise ? 1u : 0u) << (step * FB + g0 + i);
+              acc[j].add(x0, x1, wgt, m);
+            }
+          }
         }
       }
-    }
+    };
+    if (nvalid == FB)
+      bin_phase(std::true_type{});
+    else
+      bin_phase(std::false_type{});
     if (nyq_wave) {
       bool noise = false;
       if (lane < nvalid) {
         const cf* Zm = slot_ptr<N>(lds, lane);
         cf y0, y1, zr{0, 0};
-        split_pair(Zm[N / 2], Zm[N / 2], y0, y1);
+        split_pair2(Zm[N / 2], Zm[N / 2], y0, y1);
         if constexpr (MASK == MASK_IBM) zr = slot_ptr<N>(lds, FB + lane)[N / 2];
         float wn;
         const float mn = bin_mask<MASK>(A, b, y0, y1, zr, zr, N / 2, f0 + lane, noise, wn);
@@ -293,6 +324,8 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
 #pragma unroll
     for (int q = 0; q < 5; ++q) R[q] += (double)P[((long long)cc * 5 + q) * F];
   }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) R[q] *= 0.25;  // analysis accumulates (2 y)(2 y)^H
   const double* d = A.steer + 4 * k;
   cf al, be;
   float* wdbg = A.w_out ? A.w_out + ((long long)b * F + k) * 4 : nullptr;
@@ -351,10 +384,17 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(ChainArgs A
   cf v[PPL];
   auto issue_loads = [&](int step) {
     const int s0 = (t0 + step * FB + my_slot) * H - N / 2 + lm.in0;
-    static_for<0, PPL>([&](auto r) {
-      v[r].x = bload(r_m0, s0 + C::IN_STRIDE * r);
-      v[r].y = bload(r_m1, s0 + C::IN_STRIDE * r);
-    });
+    if (t0 + step * FB + wave * C::FPW >= 1) {  // wave-uniform: no negative sample index
+      static_for<0, PPL>([&](auto r) {
+        v[r].x = bload_nn(r_m0, s0 + C::IN_STRIDE * r);
+        v[r].y = bload_nn(r_m1, s0 + C::IN_STRIDE * r);
+      });
+    } else {
+      static_for<0, PPL>([&](auto r) {
+        v[r].x = bload(r_m0, s0 + C::IN_STRIDE * r);
+        v[r].y = bload(r_m1, s0 + C::IN_STRIDE * r);
+      });
+    }
   };
   AVZ_STAMP_DECL();
   AVZ_STAMP_INIT();
@@ -431,21 +471,29 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(ChainArgs A
     for (int j = 0; j < BPT; ++j) {
       const int kb = tid + j * NT;
       const int kp = (N - kb) & (N - 1);
+      // Branch-free: frames past T were transformed from zeros and get gain 0, and the
+      // OLA never writes the segments they touch, so every pair is processed.
+      cf za[NPAIR], zap[NPAIR], zb[NPAIR], zbp[NPAIR];
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p) {
+        const cf* Za = slot_ptr<N>(lds, 2 * p);
+        const cf* Zb = slot_ptr<N>(lds, 2 * p + 1);
+        za[p] = Za[kb];
+        zap[p] = Za[kp];
+        zb[p] = Zb[kb];
+        zbp[p] = Zb[kp];
+      }
 #pragma unroll
       for (int p = 0; p < NPAIR; ++p) {
         const int ta = f0 + 2 * p;
-        if (ta < T) {
-          cf* Za = slot_ptr<N>(lds, 2 * p);
-          const cf* Zb = slot_ptr<N>(lds, 2 * p + 1);
-          const int ia = step * FB + 2 * p;
-          const float ga = gain(bits[j], ia, ta, kb), gb = gain(bits[j], ia + 1, ta + 1, kb);
-          const cf za = Za[kb], zap = Za[kp], zb = Zb[kb], zbp = Zb[kp];
-          const cf sa = apply_bin(alpha[j], beta[j], za, zap, ga);
-          const cf sb = apply_bin(alpha[j], beta[j], zb, zbp, gb);
-          Za[kp] = {sa.x + sb.y, sb.x - sa.y};  // conj(Sa) + i conj(Sb) at N - k
-          // Sa + i Sb at k; at DC irfft keeps only the real parts (written last: kp == kb)
-          Za[kb] = (kb == 0) ? cf{sa.x, sb.x} : cf{sa.x - sb.y, sa.y + sb.x};
-        }
+        cf* Za = slot_ptr<N>(lds, 2 * p);
+        const int ia = step * FB + 2 * p;
+        const float ga = gain(bits[j], ia, ta, kb), gb = gain(bits[j], ia + 1, ta + 1, kb);
+        const cf sa = apply_bin(alpha[j], beta[j], za[p], zap[p], ga);
+        const cf sb = apply_bin(alpha[j], beta[j], zb[p], zbp[p], gb);
+        Za[kp] = {sa.x + sb.y, sb.x - sa.y};  // conj(Sa) + i conj(Sb) at N - k
+        // Sa + i Sb at k; at DC irfft keeps only the real parts (written last: kp == kb)
+        Za[kb] = (kb == 0) ? cf{sa.x, sb.x} : cf{sa.x - sb.y, sa.y + sb.x};
       }
     }
     if (nyq_wave && lane < NPAIR) {  // Nyquist bin: frame pair `lane`

@@ -44,6 +44,13 @@ static __device__ unsigned long long* g_stamps;
 #define AVZ_STAMP(i) (void)0
 #endif
 
+// Unchecked-sign form for a wave whose samples are all at index >= 0: the offset is a
+// plain multiple of 4 so the per-register constant folds into the instruction's
+// immediate offset (one address VGPR for all of a lane's loads).
+__device__ __forceinline__ float bload_nn(rsrc_t r, int elem) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, elem * 4, 0, 0));
+}
+
 // LDS-only barrier: leaves global loads (the next frame's prefetch) in flight.
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -126,6 +133,12 @@ struct LaneMap {
 __device__ __forceinline__ void split_pair(cf z, cf zp, cf& a, cf& b) {
   a = {0.5f * (z.x + zp.x), 0.5f * (z.y - zp.y)};
   b = {0.5f * (z.y + zp.y), 0.5f * (zp.x - z.x)};
+}
+// The same split without the 1/2 factors (2a, 2b): exact, so sums of products of it
+// are exactly 4x the sums of the halved values (the solve scales them back by 1/4).
+__device__ __forceinline__ void split_pair2(cf z, cf zp, cf& a2, cf& b2) {
+  a2 = {z.x + zp.x, z.y - zp.y};
+  b2 = {z.y + zp.y, zp.x - z.x};
 }
 // DC / Nyquist bins: both parts are real; imaginary parts are +0 (pocketfft r2c).
 __device__ __forceinline__ void split_self(cf z, cf& a, cf& b) {

@@ -53,7 +53,11 @@ struct StftArgs {
   float* Y;                   // complex64 [B][C][F][t_stride] as float2
   long long y_stride_b, y_stride_c, y_stride_f;  // in complex elements
   int max_frames;
+  int feat;                   // 0: write Y; FEAT_*: mask-model features into `F_out`
+  float* F_out;
+  long long f_sb, f_sc, f_sf, f_st;  // feature strides in floats
 };
+enum : int { FEAT_NONE = 0, FEAT_LOGMAG_IPD = 1, FEAT_TFLITE = 2 };
 
 struct ChunkSplitArgs {
   int n_items, channels, chunk;

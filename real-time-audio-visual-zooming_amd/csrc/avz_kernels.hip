@@ -13,7 +13,34 @@ namespace avz {
 // frame of the packed channel pair, then threads split the pair per bin.
 constexpr int kStftThreads = 512;
 
-template <int N>
+// Mask-model input features of one (k, t) from the two mic spectra y0, y1:
+//  FEAT_LOGMAG_IPD (full_audio_generating_pipeline/inference.py:90-94, NCHW [b][2][F][T]):
+//    c=0 log(|y0| + 1e-7), c=1 angle(y0) - angle(y1)
+//  FEAT_TFLITE (Final_pipeline/src/inference.py:198-203, 117-128, NHWC [b][F][T][4]):
+//    log_mag, sin(ipd), cos(ipd), linspace(0, 1, F)[k]
+// float32 throughout, as numpy computes them on scipy's complex64 STFT.
+template <int FEAT, int F>
+__device__ __forceinline__ void write_features(const StftArgs& A, int b, int k, int t, cf y0,
+                                               cf y1) {
+  const float lm = logf(sqrtf(y0.x * y0.x + y0.y * y0.y) + 1e-7f);
+  const float ipd = atan2f(y0.y, y0.x) - atan2f(y1.y, y1.x);
+  float* o = A.F_out + (long long)b * A.f_sb + (long long)k * A.f_sf + (long long)t * A.f_st;
+  if constexpr (FEAT == FEAT_LOGMAG_IPD) {
+    o[0] = lm;
+    o[A.f_sc] = ipd;
+  } else {
+    // np.linspace(0, 1, F, dtype=float32): k * (1/(F-1)) in fp64, last element exactly 1
+    const float fm = (k == F - 1) ? 1.0f : (float)((double)k * (1.0 / (F - 1)));
+    float s, c;
+    sincosf(ipd, &s, &c);
+    o[0] = lm;
+    o[A.f_sc] = s;
+    o[2 * A.f_sc] = c;
+    o[3 * A.f_sc] = fm;
+  }
+}
+
+template <int N, int FEAT>
 __global__ void __launch_bounds__(kStftThreads, 1) avz_stft_kernel(StftArgs A) {
   using C = KCfg<N>;
   using G = Geo<N, kStftThreads>;
@@ -66,9 +93,13 @@ __global__ void __launch_bounds__(kStftThreads, 1) avz_stft_kernel(StftArgs A) {
     const cf* Z = slot_ptr<N>(lds, f);
     cf a, c;
     split_pair(Z[k], Z[(N - k) & (N - 1)], a, c);
-    const long long o = (long long)b * A.y_stride_b + (long long)k * A.y_stride_f + t;
-    Y[o] = make_float2(a.x, a.y);
-    if (A.channels > 1) Y[o + A.y_stride_c] = make_float2(c.x, c.y);
+    if constexpr (FEAT != FEAT_NONE) {
+      write_features<FEAT, F>(A, b, k, t, a, c);
+    } else {
+      const long long o = (long long)b * A.y_stride_b + (long long)k * A.y_stride_f + t;
+      Y[o] = make_float2(a.x, a.y);
+      if (A.channels > 1) Y[o + A.y_stride_c] = make_float2(c.x, c.y);
+    }
   }
 }
 
@@ -76,9 +107,9 @@ __global__ void __launch_bounds__(kStftThreads, 1) avz_stft_kernel(StftArgs A) {
 
 using namespace avz;
 
-template <int N>
+template <int N, int FEAT>
 static int launch_stft_t(const StftArgs* a, hipStream_t st) {
-  auto kern = avz_stft_kernel<N>;
+  auto kern = avz_stft_kernel<N, FEAT>;
   const int lds = Geo<N, kStftThreads>::LDS_BYTES;
   static bool attr_done = false;
   if (!attr_done) {
@@ -96,7 +127,19 @@ static int launch_stft_t(const StftArgs* a, hipStream_t st) {
 extern "C" int avz_launch_stft(int n_fft, const StftArgs* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (a->batch <= 0) return 0;
-  if (n_fft == 1024) return launch_stft_t<1024>(a, st);
-  if (n_fft == 512) return launch_stft_t<512>(a, st);
+  switch (a->feat) {
+    case FEAT_NONE:
+      if (n_fft == 1024) return launch_stft_t<1024, FEAT_NONE>(a, st);
+      if (n_fft == 512) return launch_stft_t<512, FEAT_NONE>(a, st);
+      break;
+    case FEAT_LOGMAG_IPD:
+      if (n_fft == 1024) return launch_stft_t<1024, FEAT_LOGMAG_IPD>(a, st);
+      if (n_fft == 512) return launch_stft_t<512, FEAT_LOGMAG_IPD>(a, st);
+      break;
+    case FEAT_TFLITE:
+      if (n_fft == 1024) return launch_stft_t<1024, FEAT_TFLITE>(a, st);
+      if (n_fft == 512) return launch_stft_t<512, FEAT_TFLITE>(a, st);
+      break;
+  }
   return -4;
 }

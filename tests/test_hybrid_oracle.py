@@ -72,3 +72,17 @@ def test_chunk_table_matches_driver_loop():
     assert list(base) == [0, 9, 10, 12]
     assert list(start[:9]) == [c * 16000 for c in range(9)]
     assert list(utt) == [0] * 9 + [1] + [2] * 2 + [3] * 2
+
+
+def test_mask_features_match_reference(g_test):
+    """log-magnitude / IPD features the reference computed for chunk 0 of its driver
+    (recorded from TFLiteBeamformer.predict_mask's arguments)."""
+    mix, _, _ = triple_f32("test")
+    f = O.mask_features(mix[:, :32000])
+    assert f.dtype == np.float32
+    assert np.array_equal(f[0], g_test["chunk0_logmag"])
+    assert np.array_equal(f[1], g_test["chunk0_ipd"])
+    ft = O.mask_features(mix[:, :32000], layout="tflite")
+    assert ft.shape == (513, 64, 4)
+    assert np.array_equal(ft[..., 0], f[0])
+    assert ft[0, 0, 3] == 0.0 and ft[-1, 0, 3] == 1.0
