@@ -34,6 +34,8 @@ extern "C" {
 #define AVZ_MASK_IPD 1      /* heuristic phase mask, masked_mvdr.py:37-46                 */
 #define AVZ_MASK_EXTERNAL 2 /* caller-provided target probability M, noise = 1 - M,
                                full_audio_generating_pipeline/inference.py:99-106          */
+#define AVZ_MASK_ONES 3     /* every bin weight 1: full-signal covariance (MPDR; the SRP
+                               scan's R, scripts/debug_srp.py:56-59)                       */
 
 /* post-filters (A10) */
 #define AVZ_PF_NONE 0       /* masked_mvdr.py: none                                      */
@@ -161,6 +163,15 @@ int avz_mask_features(const avz_plan* plan, int layout, int batch, const int* le
                       const float* x, long long x_stride, long long ch_stride, float* feat,
                       long long s_b, long long s_c, long long s_f, long long s_t,
                       void* hip_stream);
+
+/* Steered response power scan, scripts/debug_srp.py:46-62 for a batch: for the
+ * angles np.linspace(angle_lo, angle_hi, n_angles) (degrees, the plan's mic_d and
+ * c_sound, debug_srp.py:17-23 geometry), P = sum over bins f_lo <= f <= f_hi and all
+ * frames of |d^H y|^2; power_db[b][i] = 10 log10(P_i) - max_j 10 log10(P_j) (device). */
+int avz_srp_scan(const avz_plan* plan, int batch, const int* len, int max_len,
+                 const float* mix, long long mix_stride, long long ch_stride, int n_angles,
+                 double angle_lo, double angle_hi, double f_lo, double f_hi, double* power_db,
+                 void* hip_stream);
 
 const char* avz_strerror(int code);
 /* Last HIP error string recorded by the library on this thread (diagnostics). */

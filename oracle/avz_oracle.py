@@ -452,6 +452,26 @@ def mask_features(y2: np.ndarray, n_fft: int = 1024, layout: str = "unet") -> np
     return np.stack([lm, np.sin(ipd), np.cos(ipd), fm], axis=-1)
 
 
+def srp_scan(y2: np.ndarray, n_fft: int = 512, d: float = D_CORE, c: float = C_SOUND,
+             fs: int = FS, f_lo: float = 200.0, f_hi: float = 4000.0, n_angles: int = 181):
+    """scripts/debug_srp.py:46-62: steered response power over linspace(0, 180, 181),
+    summed over 200 <= f <= 4000 Hz and all frames, in dB relative to the maximum."""
+    f, _, Y = stft(y2, fs=fs, nperseg=n_fft, noverlap=n_fft // 2)
+    angles = np.linspace(0, 180, n_angles)
+    sel = (f >= f_lo) & (f <= f_hi)
+    P = []
+    for a in angles:
+        th = np.deg2rad(a)
+        t1 = (d / 2) * np.cos(0) * np.cos(th - 0) / c
+        t2 = (d / 2) * np.cos(0) * np.cos(th - np.pi) / c
+        om = 2 * np.pi * f[sel]
+        dv = np.stack([np.exp(-1j * om * t1), np.exp(-1j * om * t2)])       # [2, F']
+        out = np.einsum("mf,mft->ft", dv.conj(), Y[:, sel, :])
+        P.append(np.sum(np.abs(out) ** 2))
+    P = 10 * np.log10(np.array(P))
+    return angles, P - P.max()
+
+
 def chunk_target_mask(tgt: np.ndarray, itf: np.ndarray, start: int, chunk: int = WIN_SIZE,
                       n_fft: int = 1024) -> np.ndarray:
     """Oracle target mask |S_t| >= |S_i| of one driver chunk (the stand-in for the absent

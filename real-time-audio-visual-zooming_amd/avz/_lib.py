@@ -24,7 +24,7 @@ AVZ_ERR_HIP = -3
 AVZ_ERR_UNSUPPORTED = -4
 AVZ_ERR_ALIGN = -5
 
-MASK_IBM, MASK_IPD, MASK_EXTERNAL = 0, 1, 2
+MASK_IBM, MASK_IPD, MASK_EXTERNAL, MASK_ONES = 0, 1, 2, 3
 PF_NONE, PF_IBM_TARGET, PF_EXT_FLOOR, PF_EXT_MUL = 0, 1, 2, 3
 NORM_NONE, NORM_PEAK = 0, 1
 BF_MVDR, BF_HYBRID_NULL = 0, 1
@@ -33,7 +33,7 @@ FEAT_LOGMAG_IPD, FEAT_TFLITE = 1, 2
 EXPORTED = [
     "avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
     "avz_mvdr_batch", "avz_plan_set_timing", "avz_plan_get_timing", "avz_stft",
-    "avz_chunk_split", "avz_chunk_merge", "avz_mask_features", "avz_strerror",
+    "avz_chunk_split", "avz_chunk_merge", "avz_mask_features", "avz_srp_scan", "avz_strerror",
     "avz_last_hip_error", "avz_version",
 ]
 
@@ -102,12 +102,15 @@ def _load():
     lib.avz_chunk_split.argtypes = [I, I, I, P, P, P, P, LL, LL, P, LL, LL, P]
     lib.avz_chunk_merge.argtypes = [I, I, I, I, P, P, P, LL, P, LL, P, I, ct.c_double, P]
     lib.avz_mask_features.argtypes = [P, I, I, P, I, P, LL, LL, P, LL, LL, LL, LL, P]
+    D = ct.c_double
+    lib.avz_srp_scan.argtypes = [P, I, P, I, P, LL, LL, I, D, D, D, D, P, P]
     lib.avz_strerror.argtypes = [ct.c_int]
     lib.avz_strerror.restype = ct.c_char_p
     lib.avz_last_hip_error.restype = ct.c_char_p
     for name in ("avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
                  "avz_mvdr_batch", "avz_stft", "avz_chunk_split", "avz_chunk_merge",
                  "avz_plan_set_timing", "avz_plan_get_timing", "avz_mask_features",
+                 "avz_srp_scan",
                  "avz_version"):
         getattr(lib, name).restype = ct.c_int
     return lib

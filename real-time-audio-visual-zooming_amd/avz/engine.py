@@ -16,7 +16,8 @@ import torch
 from . import _lib
 from ._lib import AvzBatchArgs, AvzConfig, check, lib
 
-MASKS = {"ibm": _lib.MASK_IBM, "ipd": _lib.MASK_IPD, "external": _lib.MASK_EXTERNAL}
+MASKS = {"ibm": _lib.MASK_IBM, "ipd": _lib.MASK_IPD, "external": _lib.MASK_EXTERNAL,
+         "ones": _lib.MASK_ONES}
 POSTFILTERS = {"none": _lib.PF_NONE, "ibm": _lib.PF_IBM_TARGET, "floor": _lib.PF_EXT_FLOOR,
                "mul": _lib.PF_EXT_MUL}
 NORMS = {"none": _lib.NORM_NONE, "peak": _lib.NORM_PEAK}
@@ -235,4 +236,25 @@ def mask_features(plan: MVDRPlan, x: torch.Tensor, layout: str = "unet", lengths
                                 ct.c_void_p(x.data_ptr()), x.stride(0), x.stride(1),
                                 ct.c_void_p(out.data_ptr()), sb, sc, sf, st,
                                 _stream_handle(stream)), "avz_mask_features")
+    return out
+
+
+def srp_scan(plan: MVDRPlan, mix: torch.Tensor, lengths=None, max_len=None, n_angles=181,
+             angle_lo=0.0, angle_hi=180.0, f_lo=200.0, f_hi=4000.0, stream=None):
+    """scripts/debug_srp.py:46-62 for a [B, 2, S] batch -> power map [B, n_angles] in dB
+    relative to each utterance's maximum (float64, device)."""
+    if mix.dim() != 3 or mix.shape[1] != 2 or mix.dtype != torch.float32 or not mix.is_cuda \
+            or mix.stride(2) != 1:
+        raise ValueError("mix must be float32 [B, 2, S] on the device")
+    B, _, S = mix.shape
+    if lengths is None:
+        lengths = torch.full((B,), S, dtype=torch.int32, device=mix.device)
+        max_len = S
+    if max_len is None:
+        max_len = int(lengths.max().item())
+    out = torch.empty((B, n_angles), dtype=torch.float64, device=mix.device)
+    check(lib.avz_srp_scan(plan._h, B, ct.c_void_p(lengths.data_ptr()), int(max_len),
+                           ct.c_void_p(mix.data_ptr()), mix.stride(0), mix.stride(1), n_angles,
+                           float(angle_lo), float(angle_hi), float(f_lo), float(f_hi),
+                           ct.c_void_p(out.data_ptr()), _stream_handle(stream)), "avz_srp_scan")
     return out

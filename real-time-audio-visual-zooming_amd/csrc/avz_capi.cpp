@@ -87,7 +87,7 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
   if (c.fs <= 0 || c.c_sound <= 0 || !(c.sigma >= 0) || c.max_batch <= 0 ||
       c.max_samples < c.n_fft)
     return AVZ_ERR_ARG;
-  if (c.mask_mode < AVZ_MASK_IBM || c.mask_mode > AVZ_MASK_EXTERNAL) return AVZ_ERR_ARG;
+  if (c.mask_mode < AVZ_MASK_IBM || c.mask_mode > AVZ_MASK_ONES) return AVZ_ERR_ARG;
   if (c.postfilter < AVZ_PF_NONE || c.postfilter > AVZ_PF_EXT_MUL) return AVZ_ERR_ARG;
   if (c.postfilter == AVZ_PF_IBM_TARGET && c.mask_mode != AVZ_MASK_IBM) return AVZ_ERR_ARG;
   if ((c.postfilter == AVZ_PF_EXT_FLOOR || c.postfilter == AVZ_PF_EXT_MUL) &&
@@ -221,6 +221,8 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   k.sigma = c.sigma;
   k.tau1 = p->tau1;
   k.tau2 = p->tau2;
+  k.mic_d = c.mic_d;
+  k.c_sound = c.c_sound;
   k.fmin_hz = c.fmin_hz;
   k.weight_eps = (float)c.weight_eps;
   k.pf_floor = (float)c.pf_floor;
@@ -393,6 +395,42 @@ extern "C" int avz_mask_features(const avz_plan* p, int layout, int batch, const
   s.f_sf = s_f;
   s.f_st = s_t;
   const int rc = avz_launch_stft(p->cfg.n_fft, &s, stream);
+  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  return rc;
+}
+
+extern "C" int avz_srp_scan(const avz_plan* p, int batch, const int* len, int max_len,
+                            const float* mix, long long mix_stride, long long ch_stride,
+                            int n_angles, double angle_lo, double angle_hi, double f_lo,
+                            double f_hi, double* power_db, void* stream) {
+  if (!p || !len || !mix || !power_db) return AVZ_ERR_ARG;
+  const avz_config& c = p->cfg;
+  if (batch < 0 || batch > c.max_batch || n_angles < 1) return AVZ_ERR_SHAPE;
+  if (batch == 0) return AVZ_OK;
+  if (max_len < c.n_fft || max_len > c.max_samples || ch_stride < max_len) return AVZ_ERR_SHAPE;
+  if (batch > 1 && mix_stride < ch_stride + max_len) return AVZ_ERR_SHAPE;
+  avz::ChainArgs k{};
+  k.batch = batch;
+  k.len = len;
+  k.mix = mix;
+  k.mix_stride = mix_stride;
+  k.ch_stride = ch_stride;
+  k.fs = c.fs;
+  k.mic_d = c.mic_d;
+  k.c_sound = c.c_sound;
+  k.max_frames = frames_for(max_len, c.hop);
+  k.nchunk = p->nchunk;
+  k.part = p->part;
+  k.mwords = p->mwords;
+  k.peak_u = p->peak_u;
+  avz::SrpArgs s{};
+  s.n_angles = n_angles;
+  s.angle_lo = angle_lo;
+  s.angle_hi = angle_hi;
+  s.f_lo = f_lo;
+  s.f_hi = f_hi;
+  s.power_db = power_db;
+  const int rc = avz_launch_srp(c.n_fft, &k, &s, stream);
   if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
   return rc;
 }

@@ -104,6 +104,9 @@ __device__ __forceinline__ float bin_mask(const ChainArgs& A, int b, cf x0, cf x
   } else if constexpr (MASK == MASK_IPD) {
     wgt = ipd_weight(x0, x1);
     return wgt;
+  } else if constexpr (MASK == MASK_ONES) {  // unmasked covariance (SRP, MPDR)
+    wgt = 1.0f;
+    return 1.0f;
   } else {
     const float M =
         A.ext_mask[(long long)b * A.mask_sb + (long long)k * A.mask_sf + (long long)t * A.mask_st];
@@ -338,6 +341,69 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
 #pragma unroll
     for (int q = 0; q < 5; ++q) A.cov_out[((long long)b * F + k) * 5 + q] = R[q];
   }
+}
+
+// ================================ SRP scan ================================
+// scripts/debug_srp.py:46-62: P(theta) = sum_{f_lo <= f_k <= f_hi} sum_t |d^H y|^2
+//   = sum_k R00 + R11 + 2 Re(conj(d0) d1 R01), conj(d0) d1 = exp(i w_k (tau1 - tau2)),
+// from the unmasked covariance partials of the analysis kernel (MASK_ONES); one block
+// per utterance: partials -> fp64 R in LDS, one thread per angle, dB relative to the max.
+constexpr int kSrpThreads = 256;
+
+template <int N>
+__global__ void __launch_bounds__(kSrpThreads) avz_srp_kernel(ChainArgs A, SrpArgs S) {
+  constexpr int H = N / 2, F = N / 2 + 1;
+  __shared__ double R[F][4];
+  __shared__ double red[kSrpThreads / 64];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int L = A.len[b];
+  double* out = S.power_db + (long long)b * S.n_angles;
+  if (L < N) {
+    for (int i = tid; i < S.n_angles; i += kSrpThreads) out[i] = __builtin_nan("");
+    return;
+  }
+  const int T = (L + H - 1) / H + 1;
+  const int nch = (T + kChunk - 1) / kChunk;
+  const float* P = A.part + (long long)b * A.nchunk * 5 * F;
+  for (int k = tid; k < F; k += kSrpThreads) {
+    double r[4] = {0, 0, 0, 0};
+    for (int cc = 0; cc < nch; ++cc) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) r[q] += (double)P[((long long)cc * 5 + q) * F + k];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) R[k][q] = 0.25 * r[q];  // analysis sums (2 y)(2 y)^H
+  }
+  __syncthreads();
+  // f_k = rfftfreq(N, 1/fs)[k]; the scanned bins
+  const double df = 1.0 / (N * (1.0 / A.fs));
+  const double step = (S.n_angles > 1) ? (S.angle_hi - S.angle_lo) / (S.n_angles - 1) : 0.0;
+  double best = -1e300;
+  for (int i = tid; i < S.n_angles; i += kSrpThreads) {
+    const double ang = (i == S.n_angles - 1 && S.n_angles > 1) ? S.angle_hi : S.angle_lo + i * step;
+    const double th = ang * (M_PI / 180.0);
+    // tau1 - tau2 = (d/2) cos(th)/c - (d/2) cos(th - pi)/c  (debug_srp.py:17-23)
+    const double t1 = (A.mic_d / 2) * cos(0.0) * cos(th - 0) / A.c_sound;
+    const double t2 = (A.mic_d / 2) * cos(0.0) * cos(th - M_PI) / A.c_sound;
+    double p = 0.0;
+    for (int k = 0; k < F; ++k) {
+      const double f = k * df;
+      if (f < S.f_lo || f > S.f_hi) continue;
+      double sn, cs;
+      sincos(2.0 * M_PI * f * (t1 - t2), &sn, &cs);
+      p += R[k][0] + R[k][1] + 2.0 * (cs * R[k][2] - sn * R[k][3]);
+    }
+    const double db = 10.0 * log10(p);
+    out[i] = db;
+    best = fmax(best, db);
+  }
+  for (int o = 32; o > 0; o >>= 1) best = fmax(best, __shfl_xor(best, o, 64));
+  if ((tid & 63) == 0) red[tid >> 6] = best;
+  __syncthreads();
+  double mx = red[0];
+#pragma unroll
+  for (int w = 1; w < kSrpThreads / 64; ++w) mx = fmax(mx, red[w]);
+  for (int i = tid; i < S.n_angles; i += kSrpThreads) out[i] -= mx;
 }
 
 // ================================ synthesis ================================
@@ -704,6 +770,29 @@ static int launch_pf(const ChainArgs* a, hipStream_t st) {
   return -4;
 }
 
+template <int N>
+static int launch_srp_t(const ChainArgs* a, const SrpArgs* s, hipStream_t st) {
+  auto k1 = avz_analysis_kernel<N, MASK_ONES>;
+  constexpr int lds = CGeo<N>::LDS_BYTES;
+  static bool attr_done = false;
+  if (!attr_done) {
+    if (!set_lds(k1, lds)) return -3;
+    attr_done = true;
+  }
+  const int nch = (a->max_frames + kChunk - 1) / kChunk;
+  if (nch > a->nchunk) return -2;
+  hipLaunchKernelGGL(k1, dim3(nch, a->batch), dim3(kCThreads), lds, st, *a);
+  hipLaunchKernelGGL(avz_srp_kernel<N>, dim3(a->batch), dim3(kSrpThreads), 0, st, *a, *s);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int avz_launch_srp(int n_fft, const ChainArgs* a, const SrpArgs* s, void* stream) {
+  if (a->batch <= 0) return 0;
+  if (n_fft == 1024) return launch_srp_t<1024>(a, s, (hipStream_t)stream);
+  if (n_fft == 512) return launch_srp_t<512>(a, s, (hipStream_t)stream);
+  return -4;
+}
+
 extern "C" int avz_launch_chunked(int n_fft, int mask_mode, const ChainArgs* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (a->batch <= 0) return 0;
@@ -712,12 +801,14 @@ extern "C" int avz_launch_chunked(int n_fft, int mask_mode, const ChainArgs* a, 
       case MASK_IBM: return launch_pf<1024, MASK_IBM>(a, st);
       case MASK_IPD: return launch_pf<1024, MASK_IPD>(a, st);
       case MASK_EXTERNAL: return launch_pf<1024, MASK_EXTERNAL>(a, st);
+      case MASK_ONES: return launch_pf<1024, MASK_ONES>(a, st);
     }
   } else if (n_fft == 512) {
     switch (mask_mode) {
       case MASK_IBM: return launch_pf<512, MASK_IBM>(a, st);
       case MASK_IPD: return launch_pf<512, MASK_IPD>(a, st);
       case MASK_EXTERNAL: return launch_pf<512, MASK_EXTERNAL>(a, st);
+      case MASK_ONES: return launch_pf<512, MASK_ONES>(a, st);
     }
   }
   return -4;

@@ -4,7 +4,7 @@
 
 namespace avz {
 
-enum : int { MASK_IBM = 0, MASK_IPD = 1, MASK_EXTERNAL = 2 };
+enum : int { MASK_IBM = 0, MASK_IPD = 1, MASK_EXTERNAL = 2, MASK_ONES = 3 };
 enum : int { PF_NONE = 0, PF_IBM_TARGET = 1, PF_EXT_FLOOR = 2, PF_EXT_MUL = 3 };
 enum : int { NORM_NONE = 0, NORM_PEAK = 1 };
 
@@ -28,6 +28,7 @@ struct ChainArgs {
   double* cov_out;            // [B][F][5] or null: sum m|y0|^2, sum m|y1|^2, Re/Im sum m y0 y1*, sum m
   float* w_out;               // [B][F][4] or null: Re w0, Im w0, Re w1, Im w1
   double fs, sigma, tau1, tau2, fmin_hz;
+  double mic_d, c_sound;
   float weight_eps, pf_floor, norm_eps;
   int postfilter, normalize;
   int beamformer;             // BF_*
@@ -59,6 +60,13 @@ struct StftArgs {
 };
 enum : int { FEAT_NONE = 0, FEAT_LOGMAG_IPD = 1, FEAT_TFLITE = 2 };
 
+struct SrpArgs {
+  int n_angles;
+  double angle_lo, angle_hi;  // np.linspace(angle_lo, angle_hi, n_angles)
+  double f_lo, f_hi;          // bins with f_lo <= f <= f_hi
+  double* power_db;           // [B][n_angles]
+};
+
 struct ChunkSplitArgs {
   int n_items, channels, chunk;
   const int* item_utt;        // [n_items] source utterance
@@ -89,6 +97,7 @@ extern "C" {
 int avz_launch_chunk_split(const avz::ChunkSplitArgs* a, void* stream);
 int avz_launch_chunk_merge(const avz::ChunkMergeArgs* a, void* stream);
 int avz_launch_chunked(int n_fft, int mask_mode, const avz::ChainArgs* a, void* stream);
+int avz_launch_srp(int n_fft, const avz::ChainArgs* a, const avz::SrpArgs* s, void* stream);
 int avz_chunk_frames(void);
 int avz_launch_stft(int n_fft, const avz::StftArgs* a, void* stream);
 }

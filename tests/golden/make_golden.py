@@ -19,7 +19,7 @@ Final_pipeline/src/inference.py imports tensorflow at module level; an empty sta
 module is injected (only TFLiteBeamformer uses it, and that class is replaced by
 _MaskFeeder below because the .tflite model file is absent).
 
-Usage:  python tests/golden/make_golden.py [hybrid]   (writes tests/golden/*.npz)
+Usage:  python tests/golden/make_golden.py [hybrid] [srp]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -263,6 +263,33 @@ def gen_final_pipeline(trip, run_metrics, save):
         save(f"hybrid_{k}.npz", **arrays)
 
 
+def gen_srp(trip, save):
+    """scripts/debug_srp.py main() on each bundled mixture; the power map is captured
+    from its plt.plot call (the script only plots it)."""
+    import debug_srp  # scripts/ (on sys.path via install_reference)
+    for k, (m, _, _) in trip.items():
+        got = {}
+        orig = debug_srp.plt.plot
+
+        def plot(*a, **kw):
+            if "x" not in got:
+                got["x"], got["y"] = np.array(a[0]), np.array(a[1])
+            return orig(*a, **kw)
+        with tempfile.TemporaryDirectory() as td:
+            world = os.path.join(td, "run", "World_Outputs")
+            os.makedirs(world)
+            wavfile.write(os.path.join(world, "mixture_3_sources.wav"), 16000, m)
+            debug_srp.plt.plot = plot
+            try:
+                with contextlib.redirect_stdout(open(os.devnull, "w")):
+                    debug_srp.main(world)
+            finally:
+                debug_srp.plt.plot = orig
+                debug_srp.plt.close("all")
+        save(f"srp_{k}.npz", angles=got["x"], power_db=got["y"], n_fft=512, mic_d=debug_srp.D,
+             c=debug_srp.C, f_lo=200.0, f_hi=4000.0)
+
+
 def main():
     od, mm, run_metrics, metrics = install_reference()
     mpath = os.path.join(HERE, "MANIFEST.json")
@@ -282,6 +309,8 @@ def main():
     if only:
         if "hybrid" in only:
             gen_final_pipeline(trip, run_metrics, save)
+        if "srp" in only:
+            gen_srp(trip, save)
         with open(mpath, "w") as fh:
             json.dump(manifest, fh, indent=1, sort_keys=True)
         return
@@ -365,6 +394,7 @@ def main():
 
     # -- Final_pipeline hybrid hard-null driver (run.py inf / batch_run) -----------
     gen_final_pipeline(trip, run_metrics, save)
+    gen_srp(trip, save)
 
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)

@@ -86,3 +86,13 @@ def test_mask_features_match_reference(g_test):
     assert ft.shape == (513, 64, 4)
     assert np.array_equal(ft[..., 0], f[0])
     assert ft[0, 0, 3] == 0.0 and ft[-1, 0, 3] == 1.0
+
+
+@pytest.mark.parametrize("trip", ["test", "set2"])
+def test_srp_scan_matches_reference(trip):
+    """scripts/debug_srp.py power map, captured from the reference's own run."""
+    g = golden(f"srp_{trip}.npz")
+    mix, _, _ = triple_f32(trip)
+    a, P = O.srp_scan(mix)
+    assert np.array_equal(a, g["angles"])
+    assert np.abs(P - g["power_db"]).max() < 1e-9
