@@ -118,6 +118,7 @@ def main():
     import torch.distributed as dist
 
     import avz
+    from avz import metrics
     from oracle import avz_oracle as O
 
     torch.cuda.set_device(local)
@@ -165,20 +166,12 @@ def main():
     # ---- final metrics: projection SIR per utterance (run_metrics.py:6-36), RCCL all-reduce
     n_out = plan.out_len(S)
     L = min(n_out, S)
-    o = out[:, :L].double()
-    t = d_tgt[:, :L].double()
-    i_ = d_itf[:, :L].double()
-    m0 = d_mix[:, 0, :L].double()
-
-    def sir(x):
-        x = x / (x.norm(dim=1, keepdim=True) + 1e-10)
-        th = t / (t.norm(dim=1, keepdim=True) + 1e-10)
-        ih = i_ / (i_.norm(dim=1, keepdim=True) + 1e-10)
-        a = (x * th).sum(1)
-        b = (x * ih).sum(1)
-        return 10 * torch.log10(a * a / (b * b + 1e-10))
-
-    sir_out, sir_in = sir(o), sir(m0)
+    # run_metrics.calculate_metrics_manual SIR of output and of mic 1, on the device
+    # (avz_projection_metrics), one call for both
+    est = torch.cat([out[:, :L], d_mix[:, 0, :L]])
+    m = metrics.projection_metrics(est, torch.cat([d_tgt[:, :L]] * 2),
+                                   torch.cat([d_itf[:, :L]] * 2))
+    sir_out, sir_in = m[:B, 3], m[B:, 3]
     sums = torch.stack([sir_in.sum(), sir_out.sum(), torch.tensor(float(B), device=dev,
                                                                   dtype=torch.float64)])
     if world > 1:

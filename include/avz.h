@@ -173,6 +173,18 @@ int avz_srp_scan(const avz_plan* plan, int batch, const int* len, int max_len,
                  double angle_lo, double angle_hi, double f_lo, double f_hi, double* power_db,
                  void* hip_stream);
 
+/* Projection metrics of a batch (device arrays, float32 signals of len[b] samples, the
+ * caller having aligned them to the minimum length as metrics.py:91-98 does):
+ * metrics[b] = { OSINR, OSIR } of Final_pipeline/src/metrics.py:102-123
+ *              (calculate_osnr_osir; output not normalised) and
+ *              { SDR, SIR } of scripts/run_metrics.py:6-36 (calculate_metrics_manual),
+ * in dB, from fp64 inner products; sums[b][6] is caller-provided workspace
+ * (<o,o>, <t,t>, <i,i>, <o,t>, <o,i>, <t,i> on return). */
+int avz_projection_metrics(int batch, int max_len, const int* len, const float* est,
+                           long long est_stride, const float* tgt, long long tgt_stride,
+                           const float* itf, long long itf_stride, double* sums,
+                           double* metrics, void* hip_stream);
+
 const char* avz_strerror(int code);
 /* Last HIP error string recorded by the library on this thread (diagnostics). */
 const char* avz_last_hip_error(void);

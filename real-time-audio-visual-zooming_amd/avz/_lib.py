@@ -33,7 +33,8 @@ FEAT_LOGMAG_IPD, FEAT_TFLITE = 1, 2
 EXPORTED = [
     "avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
     "avz_mvdr_batch", "avz_plan_set_timing", "avz_plan_get_timing", "avz_stft",
-    "avz_chunk_split", "avz_chunk_merge", "avz_mask_features", "avz_srp_scan", "avz_strerror",
+    "avz_chunk_split", "avz_chunk_merge", "avz_mask_features", "avz_srp_scan",
+    "avz_projection_metrics", "avz_strerror",
     "avz_last_hip_error", "avz_version",
 ]
 
@@ -104,13 +105,14 @@ def _load():
     lib.avz_mask_features.argtypes = [P, I, I, P, I, P, LL, LL, P, LL, LL, LL, LL, P]
     D = ct.c_double
     lib.avz_srp_scan.argtypes = [P, I, P, I, P, LL, LL, I, D, D, D, D, P, P]
+    lib.avz_projection_metrics.argtypes = [I, I, P, P, LL, P, LL, P, LL, P, P, P]
     lib.avz_strerror.argtypes = [ct.c_int]
     lib.avz_strerror.restype = ct.c_char_p
     lib.avz_last_hip_error.restype = ct.c_char_p
     for name in ("avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
                  "avz_mvdr_batch", "avz_stft", "avz_chunk_split", "avz_chunk_merge",
                  "avz_plan_set_timing", "avz_plan_get_timing", "avz_mask_features",
-                 "avz_srp_scan",
+                 "avz_srp_scan", "avz_projection_metrics",
                  "avz_version"):
         getattr(lib, name).restype = ct.c_int
     return lib

@@ -434,3 +434,30 @@ extern "C" int avz_srp_scan(const avz_plan* p, int batch, const int* len, int ma
   if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
   return rc;
 }
+
+extern "C" int avz_projection_metrics(int batch, int max_len, const int* len, const float* est,
+                                      long long est_stride, const float* tgt,
+                                      long long tgt_stride, const float* itf,
+                                      long long itf_stride, double* sums, double* metrics,
+                                      void* stream) {
+  if (batch < 0 || max_len < 0) return AVZ_ERR_SHAPE;
+  if (batch == 0) return AVZ_OK;
+  if (!len || !est || !tgt || !itf || !sums || !metrics) return AVZ_ERR_ARG;
+  if (batch > 1 && (est_stride < max_len || tgt_stride < max_len || itf_stride < max_len))
+    return AVZ_ERR_SHAPE;
+  avz::MetricsArgs m{};
+  m.batch = batch;
+  m.max_len = max_len;
+  m.len = len;
+  m.est = est;
+  m.tgt = tgt;
+  m.itf = itf;
+  m.est_stride = est_stride;
+  m.tgt_stride = tgt_stride;
+  m.itf_stride = itf_stride;
+  m.sums = sums;
+  m.metrics = metrics;
+  const int rc = avz_launch_metrics(&m, stream);
+  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  return rc;
+}

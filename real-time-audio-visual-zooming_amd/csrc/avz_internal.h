@@ -67,6 +67,17 @@ struct SrpArgs {
   double* power_db;           // [B][n_angles]
 };
 
+struct MetricsArgs {
+  int batch, max_len;
+  const int* len;             // [B] samples to score (the aligned minimum length)
+  const float* est;           // [B][est_stride] output
+  const float* tgt;           // [B][tgt_stride] target reference
+  const float* itf;           // [B][itf_stride] interference reference
+  long long est_stride, tgt_stride, itf_stride;
+  double* sums;               // [B][6] workspace
+  double* metrics;            // [B][4] OSINR, OSIR, SDR, SIR (dB)
+};
+
 struct ChunkSplitArgs {
   int n_items, channels, chunk;
   const int* item_utt;        // [n_items] source utterance
@@ -95,6 +106,7 @@ struct ChunkMergeArgs {
 
 extern "C" {
 int avz_launch_chunk_split(const avz::ChunkSplitArgs* a, void* stream);
+int avz_launch_metrics(const avz::MetricsArgs* a, void* stream);
 int avz_launch_chunk_merge(const avz::ChunkMergeArgs* a, void* stream);
 int avz_launch_chunked(int n_fft, int mask_mode, const avz::ChainArgs* a, void* stream);
 int avz_launch_srp(int n_fft, const avz::ChainArgs* a, const avz::SrpArgs* s, void* stream);

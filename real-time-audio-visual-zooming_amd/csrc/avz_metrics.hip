@@ -1,0 +1,107 @@
+// avz_metrics.hip — projection metrics of a batch on the device (gfx950).
+//
+// Final_pipeline/src/metrics.py:102-123 (calculate_osnr_osir) and
+// scripts/run_metrics.py:6-36 (calculate_metrics_manual) are projections of the output
+// onto the normalised target / interference references. Both reduce to six fp64 inner
+// products per utterance, <o,o>, <t,t>, <i,i>, <o,t>, <o,i>, <t,i>: one streaming pass
+// (float4 loads, fp64 accumulation, one atomicAdd per block and sum) and a per-utterance
+// epilogue that evaluates the reference's formulas from them.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "avz_internal.h"
+
+namespace avz {
+
+constexpr int kMetThreads = 256;
+constexpr int kMetPerThread = 16;  // samples per thread per block (4 x float4)
+
+// grid (ceil(max_len / (256 * 16)), batch)
+__global__ void __launch_bounds__(kMetThreads) avz_metrics_sums_kernel(MetricsArgs A) {
+  __shared__ double red[kMetThreads / 64][6];
+  const int b = blockIdx.y;
+  const int L = A.len[b];
+  const float* o = A.est + (long long)b * A.est_stride;
+  const float* t = A.tgt + (long long)b * A.tgt_stride;
+  const float* i = A.itf + (long long)b * A.itf_stride;
+  const long long n0 = ((long long)blockIdx.x * kMetThreads + threadIdx.x) * kMetPerThread;
+  double s[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < kMetPerThread; ++j) {
+    const long long n = n0 + j;
+    if (n < L) {
+      const double ov = o[n], tv = t[n], iv = i[n];
+      s[0] = fma(ov, ov, s[0]);
+      s[1] = fma(tv, tv, s[1]);
+      s[2] = fma(iv, iv, s[2]);
+      s[3] = fma(ov, tv, s[3]);
+      s[4] = fma(ov, iv, s[4]);
+      s[5] = fma(tv, iv, s[5]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    for (int off = 32; off > 0; off >>= 1) s[q] += __shfl_xor(s[q], off, 64);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) red[w][q] = s[q];
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    double v = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < kMetThreads / 64; ++ww) v += red[ww][threadIdx.x];
+    atomicAdd(A.sums + (long long)b * 6 + threadIdx.x, v);
+  }
+}
+
+// One thread per utterance: metrics[b] = {OSINR, OSIR, SDR, SIR} in dB.
+__global__ void avz_metrics_final_kernel(MetricsArgs A) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= A.batch) return;
+  const double* s = A.sums + (long long)b * 6;
+  const double oo = s[0], tt = s[1], ii = s[2], ot = s[3], oi = s[4], ti = s[5];
+  const double eps = 1e-10;
+  const double nt = sqrt(tt) + eps, ni = sqrt(ii) + eps, no = sqrt(oo) + eps;
+  // metrics.py:102-123: t^ = t/(|t|+eps), i^ = i/(|i|+eps); alpha = <o,t^>, beta = <o,i^>
+  {
+    const double tn2 = tt / (nt * nt), in2 = ii / (ni * ni), tin = ti / (nt * ni);
+    const double al = ot / nt, be = oi / ni;
+    const double pt = al * al * tn2, pi = be * be * in2;
+    // |o - al t^ - be i^|^2
+    const double pn = oo + pt + pi - 2.0 * al * (ot / nt) - 2.0 * be * (oi / ni) +
+                      2.0 * al * be * tin;
+    A.metrics[(long long)b * 4 + 0] = 10.0 * log10(pt / (pi + fmax(pn, 0.0) + eps));
+    A.metrics[(long long)b * 4 + 1] = 10.0 * log10(pt / (pi + eps));
+  }
+  // run_metrics.py:6-36: the output is normalised too; +1e-10 on both powers
+  {
+    const double on2 = oo / (no * no), tn2 = tt / (nt * nt), in2 = ii / (ni * ni);
+    const double tin = ti / (nt * ni);
+    const double al = ot / (no * nt), be = oi / (no * ni);
+    const double pt = al * al * tn2;
+    const double pi = be * be * in2 + 1e-10;
+    const double pa = on2 + al * al * tn2 + be * be * in2 - 2.0 * al * al - 2.0 * be * be +
+                      2.0 * al * be * tin;
+    const double pn = fmax(pa, 0.0) + 1e-10;
+    A.metrics[(long long)b * 4 + 2] = 10.0 * log10(pt / (pi + pn));
+    A.metrics[(long long)b * 4 + 3] = 10.0 * log10(pt / pi);
+  }
+}
+
+}  // namespace avz
+
+using namespace avz;
+
+extern "C" int avz_launch_metrics(const MetricsArgs* a, void* stream) {
+  if (a->batch <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(a->sums, 0, sizeof(double) * 6 * a->batch, st) != hipSuccess) return -3;
+  const long long per_block = (long long)kMetThreads * kMetPerThread;
+  const dim3 grid((unsigned)((a->max_len + per_block - 1) / per_block), a->batch);
+  if (a->max_len > 0)
+    hipLaunchKernelGGL(avz_metrics_sums_kernel, grid, dim3(kMetThreads), 0, st, *a);
+  hipLaunchKernelGGL(avz_metrics_final_kernel, dim3((a->batch + 63) / 64), dim3(64), 0, st, *a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

@@ -19,7 +19,7 @@ Final_pipeline/src/inference.py imports tensorflow at module level; an empty sta
 module is injected (only TFLiteBeamformer uses it, and that class is replaced by
 _MaskFeeder below because the .tflite model file is absent).
 
-Usage:  python tests/golden/make_golden.py [hybrid] [srp]   (writes tests/golden/*.npz)
+Usage:  python tests/golden/make_golden.py [hybrid] [srp] [report]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -290,6 +290,35 @@ def gen_srp(trip, save):
              c=debug_srp.C, f_lo=200.0, f_hi=4000.0)
 
 
+def gen_report(trip, metrics, save):
+    """Final_pipeline/src/metrics.py evaluate_run on a simulated-run folder built from the
+    test triple (stereo target/interference/mixture as simulation.py:205-211 writes them)
+    and the int16-quantised hybrid golden output as <run>_enhanced.wav."""
+    from src import config
+    m, t, i = trip["test"]
+    out = np.load(os.path.join(HERE, "hybrid_test.npz"))["out"]
+    est16 = np.clip(np.round(out.astype(np.float64) * 32768), -32768, 32767).astype(np.int16)
+    with tempfile.TemporaryDirectory() as td:
+        sim = os.path.join(td, "simulated", "golden_run")
+        res = os.path.join(td, "results", "golden_run_results")
+        os.makedirs(sim)
+        os.makedirs(res)
+        wavfile.write(os.path.join(sim, "mixture.wav"), 16000, m)
+        wavfile.write(os.path.join(sim, "target.wav"), 16000, np.stack([t, t], 1))
+        wavfile.write(os.path.join(sim, "interference.wav"), 16000, np.stack([i, i], 1))
+        wavfile.write(os.path.join(res, "golden_run_enhanced.wav"), 16000, est16)
+        old = (config.SIM_DIR, config.RESULTS_DIR)
+        config.SIM_DIR, config.RESULTS_DIR = os.path.join(td, "simulated"), os.path.join(td, "results")
+        try:
+            with contextlib.redirect_stdout(open(os.devnull, "w")):
+                metrics.evaluate_run("golden_run")
+        finally:
+            config.SIM_DIR, config.RESULTS_DIR = old
+        report = open(os.path.join(res, "report.txt")).read()
+        csv_text = open(os.path.join(td, "results", "batch_metrics.csv")).read()
+    save("report_test.npz", est16=est16, report=np.array(report), csv=np.array(csv_text))
+
+
 def main():
     od, mm, run_metrics, metrics = install_reference()
     mpath = os.path.join(HERE, "MANIFEST.json")
@@ -311,6 +340,8 @@ def main():
             gen_final_pipeline(trip, run_metrics, save)
         if "srp" in only:
             gen_srp(trip, save)
+        if "report" in only:
+            gen_report(trip, metrics, save)
         with open(mpath, "w") as fh:
             json.dump(manifest, fh, indent=1, sort_keys=True)
         return
@@ -395,6 +426,7 @@ def main():
     # -- Final_pipeline hybrid hard-null driver (run.py inf / batch_run) -----------
     gen_final_pipeline(trip, run_metrics, save)
     gen_srp(trip, save)
+    gen_report(trip, metrics, save)
 
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)

@@ -58,13 +58,62 @@ def test_ipd_mask_helper_matches_reference_semantics(gpu_device):
 
 
 def test_device_metrics_match_host(gpu_device):
+    """avz_projection_metrics (float32 signals, fp64 inner products) against the
+    reference formulas on the same float32 values (the reference reads float32 WAVs and
+    computes in float64, metrics.py:91-98)."""
     from avz import metrics
     g = golden("metrics_vectors.npz")
-    o, t, i = (torch.from_numpy(g[k])[None].to(gpu_device) for k in ("o", "t", "i"))
-    _, sir = metrics.calculate_metrics_manual(o, t, i)
-    _, osir = metrics.calculate_osnr_osir(o, t, i)
-    assert abs(float(sir[0]) - float(g["sir"])) < 1e-9
-    assert abs(float(osir[0]) - float(g["osir"])) < 1e-9
+    o, t, i = (g[k].astype(np.float32) for k in ("o", "t", "i"))
+    d = lambda a: torch.from_numpy(a)[None].to(gpu_device)  # noqa: E731
+    m = metrics.projection_metrics(d(o), d(t), d(i)).cpu().numpy()[0]
+    f = lambda a: a.astype(np.float64)  # noqa: E731
+    osinr, osir = O.osinr_osir(f(o), f(t), f(i))
+    sdr, sir = O.projection_sdr_sir(f(o), f(t), f(i))
+    np.testing.assert_allclose(m, [osinr, osir, sdr, sir], rtol=0, atol=1e-9)
+    # float32 rounding of the inputs moves the reference's own numbers by far less than
+    # the report's 0.01 dB resolution
+    assert abs(m[3] - float(g["sir"])) < 1e-4
+
+
+def test_device_metrics_ragged_batch(gpu_device):
+    from avz import metrics
+    rng = np.random.default_rng(3)
+    B, S = 5, 70001
+    o, t, i = (rng.standard_normal((B, S)).astype(np.float32) for _ in range(3))
+    o = o + 2.0 * t
+    L = [70001, 1, 4096, 33333, 12]
+    d = lambda a: torch.from_numpy(a).to(gpu_device)  # noqa: E731
+    m = metrics.projection_metrics(d(o), d(t), d(i), lengths=L).cpu().numpy()
+    for b in range(B):
+        f = lambda a: a[b, :L[b]].astype(np.float64)  # noqa: E731
+        ref = list(O.osinr_osir(f(o), f(t), f(i))) + list(O.projection_sdr_sir(f(o), f(t), f(i)))
+        np.testing.assert_allclose(m[b], ref, rtol=1e-9, atol=1e-9)
+
+
+def test_evaluate_run_report_matches_reference(gpu_device, tmp_path):
+    """metrics.evaluate_run mirror vs the report.txt / batch_metrics.csv the reference's
+    Final_pipeline/src/metrics.py wrote for the same files (Date line excluded)."""
+    from avz import metrics, wavio
+    g = golden("report_test.npz")
+    inp = golden("inputs_test.npz")
+    sim = tmp_path / "simulated" / "golden_run"
+    res = tmp_path / "results" / "golden_run_results"
+    sim.mkdir(parents=True)
+    res.mkdir(parents=True)
+    f = lambda a: a.astype(np.float64) / 32768.0  # noqa: E731
+    wavio.write(str(sim / "mixture.wav"), f(inp["mix"]), 16000)
+    wavio.write(str(sim / "target.wav"), np.stack([f(inp["tgt"])] * 2, 1), 16000)
+    wavio.write(str(sim / "interference.wav"), np.stack([f(inp["int"])] * 2, 1), 16000)
+    wavio.write(str(res / "golden_run_enhanced.wav"), f(g["est16"]), 16000)
+    metrics.evaluate_run("golden_run", sim_dir_root=str(tmp_path / "simulated"),
+                         results_dir=str(tmp_path / "results"))
+    got = (res / "report.txt").read_text().splitlines()
+    ref = str(g["report"]).splitlines()
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        if not a.startswith("Date:"):
+            assert a == b
+    assert (tmp_path / "results" / "batch_metrics.csv").read_text() == str(g["csv"])
 
 
 def test_batch_run_gpu_matches_oracle_enhancer(gpu_device):

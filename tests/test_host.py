@@ -72,3 +72,18 @@ def test_reference_surface_constants_and_steering():
         for k in (0, 7, 100, 512):
             np.testing.assert_allclose(masked_mvdr.get_steering_vector(a, g["f"][k], d, 343.0)[:, 0],
                                        g["sv"][j][k], atol=1e-15)
+
+
+def test_report_format_matches_reference():
+    """report.txt / batch_metrics.csv formats (Final_pipeline/src/metrics.py:16-44,
+    166-182) reproduced from the metric values; the golden was written by the reference's
+    own evaluate_run."""
+    from avz import metrics
+    g = golden("report_test.npz")
+    ref = str(g["report"]).splitlines()
+    m = dict(sir_b=-4.48, sinr_b=-4.48, sir_s=24.07, sinr_s=9.41, stoi=0.0, pesq_wb=0.0,
+             pesq_nb=0.0)
+    ts = ref[1].split("Date: ")[1]
+    assert metrics.format_report("golden_run", m, ts).splitlines() == ref
+    row = metrics.csv_row("golden_run", m)
+    assert ",".join(row[k] for k in metrics.CSV_HEADER) == str(g["csv"]).splitlines()[1]
