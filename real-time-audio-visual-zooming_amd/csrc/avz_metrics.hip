@@ -16,7 +16,20 @@ namespace avz {
 constexpr int kMetThreads = 256;
 constexpr int kMetPerThread = 16;  // samples per thread per block (4 x float4)
 
-// grid (ceil(max_len / (256 * 16)), batch)
+__device__ __forceinline__ void met_acc(double (&s)[6], float o, float t, float i) {
+  const double ov = o, tv = t, iv = i;
+  s[0] = fma(ov, ov, s[0]);
+  s[1] = fma(tv, tv, s[1]);
+  s[2] = fma(iv, iv, s[2]);
+  s[3] = fma(ov, tv, s[3]);
+  s[4] = fma(ov, iv, s[4]);
+  s[5] = fma(tv, iv, s[5]);
+}
+
+// grid (ceil(max_len / (256 * 16)), batch). Each block streams one 4096-sample tile of
+// the three signals; a wave's loads cover contiguous 1 KB (VEC: float4 per lane, all
+// rows 16-byte aligned) or 256 B (scalar) spans per instruction.
+template <bool VEC>
 __global__ void __launch_bounds__(kMetThreads) avz_metrics_sums_kernel(MetricsArgs A) {
   __shared__ double red[kMetThreads / 64][6];
   const int b = blockIdx.y;
@@ -24,19 +37,43 @@ __global__ void __launch_bounds__(kMetThreads) avz_metrics_sums_kernel(MetricsAr
   const float* o = A.est + (long long)b * A.est_stride;
   const float* t = A.tgt + (long long)b * A.tgt_stride;
   const float* i = A.itf + (long long)b * A.itf_stride;
-  const long long n0 = ((long long)blockIdx.x * kMetThreads + threadIdx.x) * kMetPerThread;
+  const long long tile = (long long)blockIdx.x * kMetThreads * kMetPerThread;
   double s[6] = {0, 0, 0, 0, 0, 0};
+  if constexpr (VEC) {
+    float4 ov[kMetPerThread / 4], tv[kMetPerThread / 4], iv[kMetPerThread / 4];
 #pragma unroll
-  for (int j = 0; j < kMetPerThread; ++j) {
-    const long long n = n0 + j;
-    if (n < L) {
-      const double ov = o[n], tv = t[n], iv = i[n];
-      s[0] = fma(ov, ov, s[0]);
-      s[1] = fma(tv, tv, s[1]);
-      s[2] = fma(iv, iv, s[2]);
-      s[3] = fma(ov, tv, s[3]);
-      s[4] = fma(ov, iv, s[4]);
-      s[5] = fma(tv, iv, s[5]);
+    for (int j = 0; j < kMetPerThread / 4; ++j) {
+      const long long n = tile + 4 * ((long long)j * kMetThreads + threadIdx.x);
+      if (n + 3 < L) {
+        ov[j] = *reinterpret_cast<const float4*>(o + n);
+        tv[j] = *reinterpret_cast<const float4*>(t + n);
+        iv[j] = *reinterpret_cast<const float4*>(i + n);
+      } else {
+        float a[3][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool in = n + e < L;
+          a[0][e] = in ? o[n + e] : 0.f;
+          a[1][e] = in ? t[n + e] : 0.f;
+          a[2][e] = in ? i[n + e] : 0.f;
+        }
+        ov[j] = make_float4(a[0][0], a[0][1], a[0][2], a[0][3]);
+        tv[j] = make_float4(a[1][0], a[1][1], a[1][2], a[1][3]);
+        iv[j] = make_float4(a[2][0], a[2][1], a[2][2], a[2][3]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kMetPerThread / 4; ++j) {
+      met_acc(s, ov[j].x, tv[j].x, iv[j].x);
+      met_acc(s, ov[j].y, tv[j].y, iv[j].y);
+      met_acc(s, ov[j].z, tv[j].z, iv[j].z);
+      met_acc(s, ov[j].w, tv[j].w, iv[j].w);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kMetPerThread; ++j) {
+      const long long n = tile + (long long)j * kMetThreads + threadIdx.x;
+      if (n < L) met_acc(s, o[n], t[n], i[n]);
     }
   }
 #pragma unroll
@@ -100,8 +137,16 @@ extern "C" int avz_launch_metrics(const MetricsArgs* a, void* stream) {
   if (hipMemsetAsync(a->sums, 0, sizeof(double) * 6 * a->batch, st) != hipSuccess) return -3;
   const long long per_block = (long long)kMetThreads * kMetPerThread;
   const dim3 grid((unsigned)((a->max_len + per_block - 1) / per_block), a->batch);
-  if (a->max_len > 0)
-    hipLaunchKernelGGL(avz_metrics_sums_kernel, grid, dim3(kMetThreads), 0, st, *a);
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+  const bool vec = al16(a->est) && al16(a->tgt) && al16(a->itf) &&
+                   (a->batch == 1 || (a->est_stride % 4 == 0 && a->tgt_stride % 4 == 0 &&
+                                      a->itf_stride % 4 == 0));
+  if (a->max_len > 0) {
+    if (vec)
+      hipLaunchKernelGGL(avz_metrics_sums_kernel<true>, grid, dim3(kMetThreads), 0, st, *a);
+    else
+      hipLaunchKernelGGL(avz_metrics_sums_kernel<false>, grid, dim3(kMetThreads), 0, st, *a);
+  }
   hipLaunchKernelGGL(avz_metrics_final_kernel, dim3((a->batch + 63) / 64), dim3(64), 0, st, *a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -5,7 +5,7 @@ set -o pipefail
 tag=${1:-iter}
 out=gpurun_out/$tag
 mkdir -p $out
-timeout -k 10 420 python -m pytest tests -m gpu -x -q > $out/gpu_tests.log 2>&1 || { tail -30 $out/gpu_tests.log; exit 1; }
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $out/gpu_tests.log 2>&1 || { tail -30 $out/gpu_tests.log; exit 1; }
 tail -1 $out/gpu_tests.log
 timeout -k 10 240 python bench.py --no-cpu > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
 tail -1 $out/bench.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("bench", round(d["value"]/1e9,2), "G", d["unit"], "ms/step", round(d["ms_per_step"],4))'
