@@ -42,6 +42,12 @@ extern "C" {
 #define AVZ_PF_IBM_TARGET 1 /* x (1 - mask_noise), oracle_debug.py:84-90                 */
 #define AVZ_PF_EXT_FLOOR 2  /* x max(M, floor), full_audio.../inference.py:116           */
 #define AVZ_PF_EXT_MUL 3    /* x M, Final_pipeline/src/inference.py:219                  */
+#define AVZ_PF_IRM 4        /* x sqrt(|S_t|^2 / (|S_t|^2 + |S_i|^2 + 1e-10)) from the two
+                               references (AVZ_MASK_IBM only), oracle_reverb.py:143-156   */
+
+/* weights of a bin whose loaded covariance is singular (A8) */
+#define AVZ_FALLBACK_MIC0 0 /* w = [1, 0], oracle_debug.py:78-79, masked_mvdr.py:120-122  */
+#define AVZ_FALLBACK_MEAN 1 /* w = ones/2, oracle_reverb.py:133-135                       */
 
 /* beamformers (A8 / A14) */
 #define AVZ_BF_MVDR 0       /* (R/(sum m + 1e-6) + sigma I)^-1 d, normalised; oracle_debug.py:66-79 */
@@ -77,6 +83,7 @@ typedef struct avz_config {
   double bypass_hz;  /* AVZ_BF_HYBRID_NULL: bins with f < bypass_hz pass mic 0 (200)  */
   double cond_max;   /* AVZ_BF_HYBRID_NULL: delay-and-sum above this 2-norm condition
                         number of [v_tgt, v_int] (10, inference.py:80)               */
+  int singular_fallback; /* AVZ_FALLBACK_*                                            */
 } avz_config;
 
 typedef struct avz_plan avz_plan;

@@ -293,6 +293,46 @@ def masked_mvdr_vec(y_mix, n_fft=512, hop=256, sigma=SIGMA_HEURISTIC, d=D_CORE,
     return s_out
 
 
+SIGMA_REVERB = 1e-3     # oracle_reverb.py:184 (--sigma default)
+
+
+def irm_gain(S_t: np.ndarray, S_i: np.ndarray) -> np.ndarray:
+    """Ideal-ratio-mask post-filter, oracle_reverb.py:143-156:
+    sqrt(|S_t|^2 / (|S_t|^2 + |S_i|^2 + 1e-10)) in float32 (complex64 spectra)."""
+    P_t = np.abs(S_t) ** 2
+    P_i = np.abs(S_i) ** 2
+    return np.sqrt(P_t / (P_t + P_i + 1e-10))
+
+
+def oracle_reverb_vec(y_mix, s_tgt, s_int, n_fft=512, hop=256, sigma=SIGMA_REVERB, hp=100.0,
+                      d=D_CORE, angle=ANGLE_TARGET, c=C_SOUND, fs=FS, normalize=True,
+                      return_stages=False):
+    """rt_av_zoom/core/oracle_reverb.py:41-174 minus file I/O (its input is the WPE
+    output mixture_wpe.wav; WPE itself is out of scope): IBM (:84-86), covariance
+    (:92-105), MVDR with diagonal loading sigma and the --hp cutoff, LinAlgError ->
+    ones/2 (:113-138), IRM post-filter (:143-156), s /= max|s| + 1e-9 (:164)."""
+    noverlap = n_fft - hop
+    f, _, Y = stft(y_mix, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    _, _, S_t = stft(s_tgt, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    _, _, S_i = stft(s_int, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    mask = ibm_mask_noise(S_t, S_i)
+    R = covariance_vec(Y, mask)
+    f_hz = np.arange(Y.shape[1]) * fs / n_fft          # :114 freq_hz = f_idx * FS / N_FFT
+    W = mvdr_weights_vec(R, f_hz, sigma, angle, d, c, fmin=hp)
+    a = R[:, 0, 0] + sigma
+    e = R[:, 1, 1] + sigma
+    W[(a * e - R[:, 0, 1] * R[:, 1, 0] == 0) & (f_hz >= hp)] = 0.5   # :133-135 ones/n
+    g = irm_gain(S_t, S_i)
+    S_final = apply_weights(W, Y) * g
+    _, s_raw = istft(S_final, fs=fs, nperseg=n_fft, noverlap=noverlap)
+    peak = np.max(np.abs(s_raw))
+    s_out = s_raw / (peak + 1e-9) if normalize else s_raw
+    if return_stages:
+        return s_out, dict(Y=Y, S_t=S_t, S_i=S_i, mask=mask, R=R, W=W, gain=g, s_raw=s_raw,
+                           peak=peak, f=f)
+    return s_out
+
+
 def external_mask_vec(y_mix, mask_target, n_fft=1024, hop=512, sigma=1e-5, d=0.04,
                       angle=ANGLE_TARGET, c=C_SOUND, fs=FS, floor=0.05, weight_eps=0.0,
                       normalize=False):

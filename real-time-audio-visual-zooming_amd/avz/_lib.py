@@ -25,7 +25,8 @@ AVZ_ERR_UNSUPPORTED = -4
 AVZ_ERR_ALIGN = -5
 
 MASK_IBM, MASK_IPD, MASK_EXTERNAL, MASK_ONES = 0, 1, 2, 3
-PF_NONE, PF_IBM_TARGET, PF_EXT_FLOOR, PF_EXT_MUL = 0, 1, 2, 3
+PF_NONE, PF_IBM_TARGET, PF_EXT_FLOOR, PF_EXT_MUL, PF_IRM = 0, 1, 2, 3, 4
+FALLBACK_MIC0, FALLBACK_MEAN = 0, 1
 NORM_NONE, NORM_PEAK = 0, 1
 BF_MVDR, BF_HYBRID_NULL = 0, 1
 FEAT_LOGMAG_IPD, FEAT_TFLITE = 1, 2
@@ -49,6 +50,7 @@ class AvzConfig(ct.Structure):
         ("normalize", ct.c_int), ("norm_eps", ct.c_double),
         ("max_batch", ct.c_int), ("max_samples", ct.c_int),
         ("beamformer", ct.c_int), ("bypass_hz", ct.c_double), ("cond_max", ct.c_double),
+        ("singular_fallback", ct.c_int),
     ]
 
 

@@ -19,7 +19,8 @@ from ._lib import AvzBatchArgs, AvzConfig, check, lib
 MASKS = {"ibm": _lib.MASK_IBM, "ipd": _lib.MASK_IPD, "external": _lib.MASK_EXTERNAL,
          "ones": _lib.MASK_ONES}
 POSTFILTERS = {"none": _lib.PF_NONE, "ibm": _lib.PF_IBM_TARGET, "floor": _lib.PF_EXT_FLOOR,
-               "mul": _lib.PF_EXT_MUL}
+               "mul": _lib.PF_EXT_MUL, "irm": _lib.PF_IRM}
+FALLBACKS = {"mic0": _lib.FALLBACK_MIC0, "mean": _lib.FALLBACK_MEAN}
 NORMS = {"none": _lib.NORM_NONE, "peak": _lib.NORM_PEAK}
 BEAMFORMERS = {"mvdr": _lib.BF_MVDR, "hybrid_null": _lib.BF_HYBRID_NULL}
 
@@ -54,6 +55,7 @@ class PlanConfig:
     beamformer: str = "mvdr"
     bypass_hz: float = 200.0
     cond_max: float = 10.0
+    singular_fallback: str = "mic0"
     extra: dict = field(default_factory=dict)
 
 
@@ -87,6 +89,7 @@ class MVDRPlan:
         c.max_batch, c.max_samples = cfg.max_batch, cfg.max_samples
         c.beamformer = BEAMFORMERS[cfg.beamformer]
         c.bypass_hz, c.cond_max = cfg.bypass_hz, cfg.cond_max
+        c.singular_fallback = FALLBACKS[cfg.singular_fallback]
         h = ct.c_void_p()
         check(lib.avz_plan_create(ct.byref(h), ct.byref(c)), "avz_plan_create")
         self._h = h

@@ -26,6 +26,7 @@ struct avz_plan {
   float* heads;
   float* tails;
   uint32_t* peak_u;
+  float* pf_gain;            // [max_batch][nchunk][32][F] IRM gains (AVZ_PF_IRM plans only)
   // diagnostic per-kernel timing (avz_plan_set_timing): two event sets used alternately
   bool timing;
   hipEvent_t ev[2][5];
@@ -88,8 +89,12 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
       c.max_samples < c.n_fft)
     return AVZ_ERR_ARG;
   if (c.mask_mode < AVZ_MASK_IBM || c.mask_mode > AVZ_MASK_ONES) return AVZ_ERR_ARG;
-  if (c.postfilter < AVZ_PF_NONE || c.postfilter > AVZ_PF_EXT_MUL) return AVZ_ERR_ARG;
-  if (c.postfilter == AVZ_PF_IBM_TARGET && c.mask_mode != AVZ_MASK_IBM) return AVZ_ERR_ARG;
+  if (c.postfilter < AVZ_PF_NONE || c.postfilter > AVZ_PF_IRM) return AVZ_ERR_ARG;
+  if ((c.postfilter == AVZ_PF_IBM_TARGET || c.postfilter == AVZ_PF_IRM) &&
+      c.mask_mode != AVZ_MASK_IBM)
+    return AVZ_ERR_ARG;
+  if (c.singular_fallback != AVZ_FALLBACK_MIC0 && c.singular_fallback != AVZ_FALLBACK_MEAN)
+    return AVZ_ERR_ARG;
   if ((c.postfilter == AVZ_PF_EXT_FLOOR || c.postfilter == AVZ_PF_EXT_MUL) &&
       c.mask_mode != AVZ_MASK_EXTERNAL)
     return AVZ_ERR_ARG;
@@ -117,7 +122,11 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
     const size_t sz_coef = up(sizeof(float) * B * F * 4);
     const size_t sz_ht = up(sizeof(float) * B * p->nchunk * H);
     const size_t sz_b = up(sizeof(uint32_t) * B);
-    hipError_t e = hipMalloc(&p->arena, sz_part + sz_mw + sz_steer + sz_coef + 2 * sz_ht + sz_b);
+    const size_t sz_gain = c.postfilter == AVZ_PF_IRM
+                               ? up(sizeof(float) * B * p->nchunk * avz_chunk_frames() * F)
+                               : 0;
+    hipError_t e =
+        hipMalloc(&p->arena, sz_part + sz_mw + sz_steer + sz_coef + 2 * sz_ht + sz_b + sz_gain);
     if (e != hipSuccess) {
       delete p;
       return hip_fail(e);
@@ -129,7 +138,8 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
     p->coef = reinterpret_cast<float*>(q); q += sz_coef;
     p->heads = reinterpret_cast<float*>(q); q += sz_ht;
     p->tails = reinterpret_cast<float*>(q); q += sz_ht;
-    p->peak_u = reinterpret_cast<uint32_t*>(q);
+    p->peak_u = reinterpret_cast<uint32_t*>(q); q += sz_b;
+    p->pf_gain = sz_gain ? reinterpret_cast<float*>(q) : nullptr;
     // d_m(f_k) = exp(-1j * (2 pi f_k) * tau_m), f_k = np.fft.rfftfreq(n_fft, 1/fs)[k]
     // (masked_mvdr.py:22-35); the hybrid null beamformer phase-normalises it to mic 0,
     // v / (v[0] + 1e-10) (Final_pipeline/src/inference.py:16-26).
@@ -238,6 +248,8 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   k.heads = p->heads;
   k.tails = p->tails;
   k.peak_u = p->peak_u;
+  k.pf_gain = p->pf_gain;
+  k.singular_fallback = c.singular_fallback;
   avz_plan* mp = const_cast<avz_plan*>(p);  // timing state only (diagnostic)
   void* evs[5];
   int set = -1;

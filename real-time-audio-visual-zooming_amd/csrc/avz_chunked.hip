@@ -116,6 +116,16 @@ __device__ __forceinline__ float bin_mask(const ChainArgs& A, int b, cf x0, cf x
   }
 }
 
+// IRM post-filter gain of one (bin, frame) from the packed reference pair
+// (oracle_reverb.py:143-156): with 2T, 2I the unscaled split, |2T|^2/(|2T|^2+|2I|^2+4e-10)
+// equals P_t/(P_t + P_i + 1e-10).
+__device__ __forceinline__ float irm_gain(cf zr, cf zrp) {
+  const float tr = zr.x + zrp.x, ti = zr.y - zrp.y;
+  const float ir = zr.y + zrp.y, ii = zr.x - zrp.x;
+  const float pt = tr * tr + ti * ti, pi = ir * ir + ii * ii;
+  return sqrtf(pt / (pt + pi + 4e-10f));
+}
+
 // ================================ analysis ================================
 template <int N, int MASK>
 __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A) {
@@ -187,6 +197,10 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A)
     acc[j].zero();
     bits[j] = 0u;
   }
+  // IRM post-filter gains of this chunk (PF_IRM plans only; block-uniform)
+  float* const gain = (MASK == MASK_IBM && A.pf_gain)
+                          ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F
+                          : nullptr;
   // Nyquist bin N/2: frame `lane` of each step on the last wave's lanes.
   const bool nyq_wave = (wave == G::NWAVE - 1);
   Acc32 an;
@@ -245,6 +259,9 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A)
                   bin_mask<MASK>(A, b, x0, x1, zr[i], zrp[i], kb, f0 + g0 + i, noise, wgt);
               bits[j] |= (noise ? 1u : 0u) << (step * FB + g0 + i);
               acc[j].add(x0, x1, wgt, m);
+              if constexpr (MASK == MASK_IBM) {
+                if (gain) gain[(step * FB + g0 + i) * F + kb] = irm_gain(zr[i], zrp[i]);
+              }
             }
           }
         }
@@ -264,6 +281,9 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A)
         float wn;
         const float mn = bin_mask<MASK>(A, b, y0, y1, zr, zr, N / 2, f0 + lane, noise, wn);
         an.add(y0, y1, wn, mn);
+        if constexpr (MASK == MASK_IBM) {
+          if (gain) gain[(step * FB + lane) * F + N / 2] = irm_gain(zr, zr);
+        }
       }
       const unsigned long long bal = __ballot(noise);
       nyq_bits |= ((uint32_t)bal & ((1u << FB) - 1u)) << (step * FB);
@@ -487,10 +507,14 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(ChainArgs A
     beta_n = cf{cw.z, cw.w};
     if (PF == PF_IBM_TARGET) bits_n = MW[N / 2];
   }
+  const float* irm = (PF == PF_IRM) ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F
+                                    : nullptr;
   auto gain = [&](uint32_t bb, int i, int t, int k) -> float {  // i: frame bit in chunk
     if (t >= T) return 0.0f;
     if constexpr (PF == PF_IBM_TARGET) {
       return ((bb >> i) & 1u) ? 0.0f : 1.0f;
+    } else if constexpr (PF == PF_IRM) {
+      return irm[i * F + k];
     } else if constexpr (PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) {
       const float M =
           A.ext_mask[(long long)b * A.mask_sb + (long long)k * A.mask_sf + (long long)t * A.mask_st];
@@ -761,6 +785,7 @@ template <int N, int MASK>
 static int launch_pf(const ChainArgs* a, hipStream_t st) {
   if constexpr (MASK == MASK_IBM) {
     if (a->postfilter == PF_IBM_TARGET) return launch_chunked_t<N, MASK, PF_IBM_TARGET>(a, st);
+    if (a->postfilter == PF_IRM) return launch_chunked_t<N, MASK, PF_IRM>(a, st);
   }
   if constexpr (MASK == MASK_EXTERNAL) {
     if (a->postfilter == PF_EXT_FLOOR) return launch_chunked_t<N, MASK, PF_EXT_FLOOR>(a, st);

@@ -200,7 +200,7 @@ __device__ __forceinline__ void coef_from_w(double w0r, double w0i, double w1r, 
 
 // Per-bin MVDR solve in fp64 (oracle_debug.py:66-79):
 //   w~ = (R/(sum m + 1e-6) + sigma I)^{-1} d ; w = w~ / (d^H w~ + 1e-10);
-//   singular -> w = [1, 0]; f < fmin -> w = 0.
+//   singular -> w = [1, 0] (or ones/2, oracle_reverb.py:133-135); f < fmin -> w = 0.
 // d = steering vector (masked_mvdr.py:22-35). c = {sum m|y0|^2, sum m|y1|^2,
 // Re/Im sum m y0 conj(y1), sum m}.
 __device__ __forceinline__ void mvdr_solve_d(const double (&c)[5], int k, int n_fft,
@@ -215,7 +215,12 @@ __device__ __forceinline__ void mvdr_solve_d(const double (&c)[5], int k, int n_
     const double br = c[2] / nrm, bi = c[3] / nrm;
     const double det = a * e - (br * br + bi * bi);
     if (det == 0.0 || !isfinite(det)) {
-      w0r = 1.0;
+      if (A.singular_fallback) {  // oracle_reverb.py:133-135: ones(n)/n
+        w0r = 0.5;
+        w1r = 0.5;
+      } else {  // oracle_debug.py:78-79: [1, 0]
+        w0r = 1.0;
+      }
     } else {
       // w~0 = (e d0 - b d1)/det ; w~1 = (a d1 - conj(b) d0)/det
       double t0r = e * d0r - (br * d1r - bi * d1i);

@@ -5,7 +5,7 @@
 namespace avz {
 
 enum : int { MASK_IBM = 0, MASK_IPD = 1, MASK_EXTERNAL = 2, MASK_ONES = 3 };
-enum : int { PF_NONE = 0, PF_IBM_TARGET = 1, PF_EXT_FLOOR = 2, PF_EXT_MUL = 3 };
+enum : int { PF_NONE = 0, PF_IBM_TARGET = 1, PF_EXT_FLOOR = 2, PF_EXT_MUL = 3, PF_IRM = 4 };
 enum : int { NORM_NONE = 0, NORM_PEAK = 1 };
 
 enum : int { BF_MVDR = 0, BF_HYBRID_NULL = 1 };
@@ -43,6 +43,8 @@ struct ChainArgs {
   float* heads;               // [B][nchunk][H] chunk's first frame, first-half contribution
   float* tails;               // [B][nchunk][H] chunk's last frame, second-half contribution
   uint32_t* peak_u;           // [B] max |out| over chunk interiors (float bits, atomicMax)
+  float* pf_gain;             // [B][nchunk][32][F] IRM post-filter gain (PF_IRM) or null
+  int singular_fallback;      // 0: w = [1, 0]; 1: w = [1/2, 1/2]
   void* const* events;        // host-only: 5 hipEvent_t recorded around the 4 launches, or null
 };
 

@@ -19,7 +19,8 @@ Final_pipeline/src/inference.py imports tensorflow at module level; an empty sta
 module is injected (only TFLiteBeamformer uses it, and that class is replaced by
 _MaskFeeder below because the .tflite model file is absent).
 
-Usage:  python tests/golden/make_golden.py [hybrid] [srp] [report]   (writes tests/golden/*.npz)
+Usage:  python tests/golden/make_golden.py [hybrid] [srp] [report] [reverb]
+        (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -290,6 +291,44 @@ def gen_srp(trip, save):
              c=debug_srp.C, f_lo=200.0, f_hi=4000.0)
 
 
+def run_oracle_reverb(orv, mix16, tgt16, int16_, n_fft, sigma, hp):
+    """Run rt_av_zoom/core/oracle_reverb.py main(args) (:41-174) on int16 arrays. Its
+    input is the WPE output mixture_wpe.wav; WPE (nara_wpe) is absent and out of scope,
+    so the bundled mixture is handed over under that name. Returns (out, rec)."""
+    with tempfile.TemporaryDirectory() as td:
+        wavfile.write(os.path.join(td, "mixture_wpe.wav"), 16000, mix16)
+        wavfile.write(os.path.join(td, "target_reference.wav"), 16000, tgt16)
+        wavfile.write(os.path.join(td, "interference_reference.wav"), 16000, int16_)
+        orv.N_FFT, orv.N_HOP = n_fft, n_fft // 2
+        _WRITES.clear()
+        args = types.SimpleNamespace(outdir=td, sigma=sigma, hp=hp)
+        with contextlib.redirect_stdout(open(os.devnull, "w")), capture() as rec:
+            orv.main(args)
+        return _WRITES["output_oracle_reverb.wav"], rec
+
+
+def gen_reverb(trip, run_metrics, save):
+    from rt_av_zoom.core import oracle_reverb as orv
+    cases = [(512, 1e-3, 100.0), (512, 1e-7, 200.0), (1024, 1e-3, 100.0)]
+    for k, (m, t, i) in trip.items():
+        tf = t.astype(np.float32) / 32768.0
+        itf = i.astype(np.float32) / 32768.0
+        for n, s, hp in cases:
+            out, rec = run_oracle_reverb(orv, m, t, i, n, s, hp)
+            L = min(len(out), len(tf))
+            _, sir_o = run_metrics.calculate_metrics_manual(out[:L], tf[:L], itf[:L])
+            save(f"reverb_{k}_n{n}_s{s:g}_hp{hp:g}.npz", n_fft=n, hop=n // 2, sigma=s, hp=hp,
+                 out_len=len(out), out_stride16=out[::16].astype(np.float32),
+                 out_head=out[:4096].astype(np.float32), sumsq=np.sum(out ** 2),
+                 peak_raw=np.max(np.abs(rec["istft"][0])), sir_out=sir_o)
+    seg = slice(40000, 64000)
+    m, t, i = trip["test"]
+    out, rec = run_oracle_reverb(orv, m[seg], t[seg], i[seg], 512, 1e-3, 100.0)
+    save("reverb_excerpt_test_n512.npz", seg=np.array([seg.start, seg.stop]), n_fft=512,
+         sigma=1e-3, hp=100.0, out=out.astype(np.float32),
+         S_final=rec["istft_in"].astype(np.complex128))
+
+
 def gen_report(trip, metrics, save):
     """Final_pipeline/src/metrics.py evaluate_run on a simulated-run folder built from the
     test triple (stereo target/interference/mixture as simulation.py:205-211 writes them)
@@ -342,6 +381,8 @@ def main():
             gen_srp(trip, save)
         if "report" in only:
             gen_report(trip, metrics, save)
+        if "reverb" in only:
+            gen_reverb(trip, run_metrics, save)
         with open(mpath, "w") as fh:
             json.dump(manifest, fh, indent=1, sort_keys=True)
         return
@@ -427,6 +468,7 @@ def main():
     gen_final_pipeline(trip, run_metrics, save)
     gen_srp(trip, save)
     gen_report(trip, metrics, save)
+    gen_reverb(trip, run_metrics, save)
 
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)

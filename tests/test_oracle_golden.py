@@ -113,6 +113,41 @@ def test_masked_mvdr_ipd(trip, n):
     np.testing.assert_allclose(O.masked_mvdr_vec(mix_e, n_fft=n, hop=n // 2), ge["out"], atol=5e-6)
 
 
+REVERB = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "reverb_*_hp*.npz")))
+
+
+def test_reverb_fixture_inventory():
+    assert len(REVERB) == 6
+
+
+@pytest.mark.parametrize("name", REVERB)
+def test_oracle_reverb_full_length(name):
+    """oracle_reverb.py:41-174 (IRM post-filter, --sigma/--hp) vs the reference run."""
+    g = golden(name)
+    trip = name.split("_")[1]
+    mix, tgt, itf = triple_f32(trip)
+    n, s, hp = int(g["n_fft"]), float(g["sigma"]), float(g["hp"])
+    out, st = O.oracle_reverb_vec(mix, tgt, itf, n_fft=n, hop=n // 2, sigma=s, hp=hp,
+                                  return_stages=True)
+    assert len(out) == int(g["out_len"])
+    np.testing.assert_allclose(out[::16], g["out_stride16"], atol=2e-7)
+    np.testing.assert_allclose(out[:4096], g["out_head"], atol=2e-7)
+    assert abs(st["peak"] - float(g["peak_raw"])) <= 1e-9 * float(g["peak_raw"])
+    L = min(len(out), len(tgt))
+    _, sir = O.projection_sdr_sir(out[:L], tgt[:L], itf[:L])
+    assert abs(sir - float(g["sir_out"])) < 1e-6
+
+
+def test_oracle_reverb_excerpt_spectrum():
+    g = golden("reverb_excerpt_test_n512.npz")
+    mix, tgt, itf = triple_f32("test", g["seg"])
+    out, st = O.oracle_reverb_vec(mix, tgt, itf, n_fft=512, hop=256, sigma=float(g["sigma"]),
+                                  hp=float(g["hp"]), return_stages=True)
+    S = O.apply_weights(st["W"], st["Y"]) * st["gain"]
+    np.testing.assert_allclose(S, g["S_final"], rtol=1e-9, atol=1e-15)
+    np.testing.assert_allclose(out, g["out"], atol=2e-7)
+
+
 def test_metric_vectors():
     g = golden("metrics_vectors.npz")
     sdr, sir = O.projection_sdr_sir(g["o"], g["t"], g["i"])
