@@ -353,6 +353,28 @@ def external_mask_vec(y_mix, mask_target, n_fft=1024, hop=512, sigma=1e-5, d=0.0
     return s_raw
 
 
+def neural_deploy_vec(y: np.ndarray, masks, chunk: int = 32000, n_fft: int = 1024,
+                      d: float = 0.04, sigma: float = 1e-5) -> np.ndarray:
+    """full_audio_generating_pipeline/inference.py:120-167 (main_deploy minus file I/O and
+    the model): y [S, 2]; masks[c] is the target mask of chunk c (the U-Net output);
+    each chunk through external_mask_vec (process_chunk, :88-118), the first
+    min(len(out), chunk) samples overlap-added at c * chunk/2, divided by the count."""
+    hop = chunk // 2
+    S = y.shape[0]
+    out_buf = np.zeros(S + chunk)
+    norm_buf = np.zeros(S + chunk)
+    for c in range(int(np.ceil(S / hop))):
+        seg = y[c * hop:c * hop + chunk]
+        if len(seg) < chunk:
+            seg = np.pad(seg, ((0, chunk - len(seg)), (0, 0)))
+        o = external_mask_vec(seg.T, masks[c], n_fft=n_fft, hop=n_fft // 2, sigma=sigma, d=d)
+        L = min(len(o), chunk)
+        out_buf[c * hop:c * hop + L] += o[:L]
+        norm_buf[c * hop:c * hop + L] += 1.0
+    norm_buf[norm_buf == 0] = 1.0
+    return out_buf[:S] / norm_buf[:S]
+
+
 # ----------------------------------------------------------------------------
 # Final_pipeline: hybrid hard-null beamformer + 2-s chunked overlap-add driver
 # ----------------------------------------------------------------------------

@@ -19,7 +19,7 @@ Final_pipeline/src/inference.py imports tensorflow at module level; an empty sta
 module is injected (only TFLiteBeamformer uses it, and that class is replaced by
 _MaskFeeder below because the .tflite model file is absent).
 
-Usage:  python tests/golden/make_golden.py [hybrid] [srp] [report] [reverb]
+Usage:  python tests/golden/make_golden.py [hybrid] [srp] [report] [reverb] [neural]
         (writes tests/golden/*.npz)
 """
 from __future__ import annotations
@@ -329,6 +329,91 @@ def gen_reverb(trip, run_metrics, save):
          S_final=rec["istft_in"].astype(np.complex128))
 
 
+UNET_SEED = 20250101
+
+
+def unet_checksum(state_dict):
+    """(count, sum |p|, sum p * index-weight) of a state_dict in fp64: pins the weights."""
+    n, s1, s2 = 0, 0.0, 0.0
+    for k in sorted(state_dict):
+        v = state_dict[k].detach().double().flatten().numpy()
+        n += v.size
+        s1 += float(np.abs(v).sum())
+        s2 += float((v * np.linspace(1.0, 2.0, v.size)).sum())
+    return np.array([n, s1, s2])
+
+
+def gen_neural(trip, run_metrics, save):
+    """full_audio_generating_pipeline/inference.py main_deploy (:120-167) + process_chunk
+    (:88-118). The trained weights mask_3.pth are absent upstream (.MISSING_LARGE_BLOBS:2),
+    so the reference's own FreqPreservingUNet (:29-67) is built with random init under
+    torch.manual_seed(UNET_SEED), eval mode, and saved as mask_3.pth for main_deploy to
+    load. mir_eval (imported at :10, used only by code main_deploy does not call) is
+    absent: an empty stand-in module is injected. The module reads config.json from the
+    working directory at import (:15-16); the reference's own config.json is copied there."""
+    import importlib
+
+    import torch
+    me = types.ModuleType("mir_eval")
+    me.separation = types.SimpleNamespace(bss_eval_sources=None)
+    sys.modules.setdefault("mir_eval", me)
+    sys.modules.setdefault("mir_eval.separation", me.separation)
+    pipe = os.path.join(REF, "rt_av_zoom", "core", "full_audio_generating_pipeline")
+    with tempfile.TemporaryDirectory() as td:
+        shutil.copy(os.path.join(pipe, "config.json"), td)
+        cwd = os.getcwd()
+        os.chdir(td)
+        try:
+            inf = importlib.import_module("rt_av_zoom.core.full_audio_generating_pipeline.inference")
+            torch.manual_seed(UNET_SEED)
+            model = inf.FreqPreservingUNet()
+            sd = model.state_dict()
+            torch.save(sd, "mask_3.pth")
+            conf = json.load(open("config.json"))
+            rec = {"X": [], "M": []}
+            orig_fwd = inf.FreqPreservingUNet.forward
+
+            def fwd(self, x):
+                m = orig_fwd(self, x)
+                rec["X"].append(x.detach().numpy().copy())
+                rec["M"].append(m.detach().numpy().copy())
+                return m
+
+            def deploy(mix16):
+                wavfile.write("input.wav", 16000, mix16)
+                rec["X"].clear()
+                rec["M"].clear()
+                _WRITES.clear()
+                inf.FreqPreservingUNet.forward = fwd
+                try:
+                    with contextlib.redirect_stdout(open(os.devnull, "w")):
+                        inf.main_deploy("input.wav")
+                finally:
+                    inf.FreqPreservingUNet.forward = orig_fwd
+                return _WRITES["enhanced_input.wav"]
+
+            common = dict(seed=UNET_SEED, checksum=unet_checksum(sd),
+                          keys=np.array(sorted(sd)), n_fft=conf["n_fft"], hop=conf["hop_len"],
+                          mic_d=conf["d"], chunk=conf["train_seg_samples"], sigma=inf.SIGMA)
+            for k, (m, t, i) in trip.items():
+                out = deploy(m)
+                tf = t.astype(np.float32) / 32768.0
+                itf = i.astype(np.float32) / 32768.0
+                L = min(len(out), len(tf))
+                _, sir_o = run_metrics.calculate_metrics_manual(out[:L], tf[:L], itf[:L])
+                save(f"neural_{k}.npz", **common, out_len=len(out),
+                     out_stride16=out[::16].astype(np.float32), out_head=out[:4096].astype(np.float32),
+                     sumsq=np.sum(out ** 2), sir_out=sir_o, n_chunks=len(rec["M"]))
+            seg = slice(40000, 88000)
+            m, _, _ = trip["test"]
+            out = deploy(m[seg])
+            save("neural_excerpt_test.npz", **common, seg=np.array([seg.start, seg.stop]),
+                 out=out.astype(np.float32), masks=np.concatenate(rec["M"]).astype(np.float32),
+                 feat0=rec["X"][0][0].astype(np.float32))
+        finally:
+            os.chdir(cwd)
+
+
 def gen_report(trip, metrics, save):
     """Final_pipeline/src/metrics.py evaluate_run on a simulated-run folder built from the
     test triple (stereo target/interference/mixture as simulation.py:205-211 writes them)
@@ -383,6 +468,8 @@ def main():
             gen_report(trip, metrics, save)
         if "reverb" in only:
             gen_reverb(trip, run_metrics, save)
+        if "neural" in only:
+            gen_neural(trip, run_metrics, save)
         with open(mpath, "w") as fh:
             json.dump(manifest, fh, indent=1, sort_keys=True)
         return
@@ -469,6 +556,7 @@ def main():
     gen_srp(trip, save)
     gen_report(trip, metrics, save)
     gen_reverb(trip, run_metrics, save)
+    gen_neural(trip, run_metrics, save)
 
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)
