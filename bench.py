@@ -1,17 +1,28 @@
 """Headline benchmark: beamformed TF-bins/s of the MVDR hot path on MI355X.
 
-Workload (BASELINE.json configs[1]): per GPU a batch of B = 256 synthetic 2-mic
-utterances of 4.0 s (64000 samples @ 16 kHz), 2 interferers, oracle IBM mask,
-1024-pt STFT / hop 512 -> F x T = 513 x 126 = 64,638 TF-bins per utterance.
-One step = one avz_mvdr_batch call over the whole batch: the analysis (STFT -> IBM ->
-masked covariance partials), solve (fp64 MVDR), synthesis (STFT -> apply + IBM
-post-filter -> iSTFT/OLA) and finalize (chunk seams, peak normalisation) kernels,
-inputs resident in HBM. Per-kernel times come from HIP events the plan records
-around each launch on the launch stream (avz_plan_set_timing). Multi-GPU: one process per GPU, utterances
-sharded (weak scaling, no data-path collective); the only collective is the final
-RCCL all-reduce of the SIR metric sums (and the max-over-ranks step time).
+Default workload (BASELINE.json configs[1], the one the metric is quoted on): per GPU a
+batch of B = 256 synthetic 2-mic utterances of 4.0 s (64000 samples @ 16 kHz),
+2 interferers, oracle IBM mask, 1024-pt STFT / hop 512 -> F x T = 513 x 126 = 64,638
+TF-bins per utterance. One step = one avz_mvdr_batch call over the whole batch: the
+analysis (STFT -> IBM -> masked covariance partials), solve (fp64 MVDR), synthesis
+(STFT -> apply + IBM post-filter -> iSTFT/OLA) and finalize (chunk seams, peak
+normalisation) kernels, inputs resident in HBM. Per-kernel times come from HIP events
+the plan records around each launch on the launch stream (avz_plan_set_timing).
+Multi-GPU: one process per GPU, utterances sharded (weak scaling, no data-path
+collective); the only collectives are the final RCCL all-reduce of the SIR metric sums
+and the max-over-ranks step time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+Other workloads (parity configs, measured on request, same JSON line):
+  --workload ipd   configs[3]: heuristic IPD mask (masked_mvdr.py), B = 1024, no
+                   post-filter, sigma 1e-7, s /= max|s| + 1e-6
+  --workload unet  configs[4]: 2-s chunks of B = 1024 utterances (4096 items) ->
+                   device features -> FreqPreservingUNet (PyTorch-ROCm fp32, random
+                   init: weights absent upstream) -> external-mask MVDR chain ->
+                   chunk overlap-add (main_deploy); value counts chunk TF-bins
+                   (4096 x 513 x 64) end to end, U-Net included; the U-Net and the
+                   MVDR chain are also timed alone
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload W]
        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 """
 from __future__ import annotations
@@ -33,6 +44,15 @@ import numpy as np  # noqa: E402
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 N_FFT, HOP, FS, SECONDS = 1024, 512, 16000, 4.0
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
+DEFAULT_BATCH = {"ibm": 256, "ipd": 1024, "unet": 1024}
+WORKLOAD_TEXT = {
+    "ibm": "configs[1]: B={B} utterances/GPU, {k} interferers, oracle IBM, 1024-pt STFT hop 512 "
+           "@16 kHz, 4.0 s utterances",
+    "ipd": "configs[3]: B={B} utterances/GPU, heuristic IPD mask (masked_mvdr.py), {k} "
+           "interferers, 1024-pt STFT hop 512 @16 kHz, 4.0 s utterances",
+    "unet": "configs[4]: B={B} utterances/GPU -> 2-s chunks, U-Net mask (PyTorch-ROCm fp32, "
+            "random init) -> external-mask MVDR, 1024-pt STFT hop 512, chunk OLA",
+}
 
 
 def parse():
@@ -40,7 +60,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="utterances per GPU")
+    ap.add_argument("--workload", choices=sorted(DEFAULT_BATCH), default="ibm")
+    ap.add_argument("--batch", type=int, default=0, help="utterances per GPU (0: workload default)")
     ap.add_argument("--interferers", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="time box of the CPU baseline workers")
@@ -48,7 +69,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-kernel HIP events (roofline from the step events)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.batch = a.batch or DEFAULT_BATCH[a.workload]
+    return a
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -56,7 +79,7 @@ _CPU_SAMPLE = None
 
 
 def _cpu_worker(args):
-    wid, budget = args
+    wid, budget, workload = args
     from threadpoolctl import threadpool_limits
 
     from oracle import avz_oracle as O
@@ -67,31 +90,95 @@ def _cpu_worker(args):
     with threadpool_limits(1):
         while time.perf_counter() - t0 < budget:
             b = (wid + n) % mix.shape[0]
-            O.oracle_debug_loop(mix[b], tgt[b], itf[b], n_fft=N_FFT, hop=HOP, sigma=1.0)
+            if workload == "ipd":
+                O.masked_mvdr_vec(mix[b], n_fft=N_FFT, hop=HOP)
+            else:
+                O.oracle_debug_loop(mix[b], tgt[b], itf[b], n_fft=N_FFT, hop=HOP, sigma=1.0)
             bins += (N_FFT // 2 + 1) * O.n_frames(mix.shape[-1], N_FFT, HOP)
             n += 1
     return n, bins, time.perf_counter() - t0
 
 
-def cpu_baseline(sample, seconds, workers):
-    """The loop-faithful oracle_debug restatement (oracle/avz_oracle.py, kind 'port')
-    on the host cores, time-boxed, one single-threaded worker process per core."""
+def cpu_baseline(sample, seconds, workers, workload):
+    """The oracle restatement of the same path (oracle/avz_oracle.py, kind 'port') on the
+    host cores, time-boxed, one single-threaded worker process per core: the
+    loop-faithful oracle_debug (ibm) or the vectorised masked_mvdr (ipd)."""
     import multiprocessing as mp
     global _CPU_SAMPLE
     _CPU_SAMPLE = sample
     ctx = mp.get_context("fork")  # forked before any GPU initialisation
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
-        res = pool.map(_cpu_worker, [(w, seconds) for w in range(workers)])
+        res = pool.map(_cpu_worker, [(w, seconds, workload) for w in range(workers)])
     wall = time.perf_counter() - t0
     utts = sum(r[0] for r in res)
     bins = sum(r[1] for r in res)
+    what = ("vectorised restatement of masked_mvdr.main (IPD mask, sigma 1e-7)"
+            if workload == "ipd" else
+            "loop-faithful restatement of oracle_debug.main (oracle IBM, sigma 1)")
     return {"value": bins / max(r[2] for r in res), "unit": "TF-bins/s", "cores": workers,
             "kind": "port",
             "sample": (f"time-boxed {seconds:.0f} s x {workers} single-threaded workers over "
-                       f"{sample[0].shape[0]} distinct configs[1] utterances (4.0 s, 1024/512, "
-                       f"oracle IBM, sigma 1): {utts} utterances; loop-faithful restatement of "
-                       f"oracle_debug.main minus WAV I/O; wall {wall:.1f} s")}
+                       f"{sample[0].shape[0]} distinct utterances of the same workload (4.0 s, "
+                       f"1024/512): {utts} utterances; {what} minus WAV I/O; wall {wall:.1f} s")}
+
+
+# ----------------------------------------------------------------------------- workloads
+def setup_chain(args, B, S, dev, mix, tgt, itf):
+    """ibm / ipd: one avz_mvdr_batch call per step."""
+    import torch
+
+    import avz
+    if args.workload == "ibm":
+        plan = avz.MVDRPlan(n_fft=N_FFT, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
+                            normalize="peak", max_batch=B, max_samples=S)
+        streams = 4
+    else:
+        plan = avz.MVDRPlan(n_fft=N_FFT, sigma=1e-7, mic_d=0.01, mask="ipd", postfilter="none",
+                            normalize="peak", norm_eps=1e-6, max_batch=B, max_samples=S)
+        streams = 2
+    d_mix = torch.from_numpy(mix).to(dev)
+    refs = {}
+    if args.workload == "ibm":
+        refs = dict(ref_tgt=torch.from_numpy(tgt).to(dev), ref_int=torch.from_numpy(itf).to(dev))
+    lens = torch.full((B,), S, dtype=torch.int32, device=dev)
+    out = plan.alloc_out(B, S, dev)
+    peak = torch.empty((B,), dtype=torch.float32, device=dev)
+
+    def step():
+        plan.run(d_mix, lens, max_len=S, out=out, peak=peak, **refs)
+
+    n_out = plan.out_len(S)
+    F, T = N_FFT // 2 + 1, -(-S // HOP) + 1
+    info = dict(plan=plan, out=out[:, :min(n_out, S)], bins=B * F * T,
+                alg_analysis=B * streams * S * 4, alg_chain=B * (streams * S * 4 + n_out * 4),
+                kernel=f"avz_analysis_kernel<1024,{'IBM' if args.workload == 'ibm' else 'IPD'}>",
+                mix=d_mix)
+    return step, info
+
+
+def setup_unet(args, B, S, dev, mix):
+    import torch
+
+    from avz import neural as N
+    torch.manual_seed(20250101)
+    model = N.FreqPreservingUNet().eval().to(dev)
+    n_items = B * -(-S // 16000)
+    bf = N.NeuralMaskBeamformer(model, max_items=n_items)
+    d_mix = torch.from_numpy(mix).to(dev)
+    y = {}
+
+    def step():
+        y["out"], _ = bf.run(d_mix)
+
+    F = N_FFT // 2 + 1
+    Tc = -(-bf.chunk // HOP) + 1
+    n_out = bf.plan.out_len(bf.chunk)
+    info = dict(plan=bf.plan, bf=bf, bins=n_items * F * Tc, n_items=n_items,
+                alg_analysis=n_items * 2 * bf.chunk * 4,
+                alg_chain=n_items * (2 * bf.chunk * 4 + n_out * 4),
+                kernel="avz_analysis_kernel<1024,EXTERNAL>", mix=d_mix, y=y)
+    return step, info
 
 
 def main():
@@ -109,15 +196,14 @@ def main():
                                      n_interferers=args.interferers)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and args.workload != "unet":
         workers = args.cpu_workers or min(16, len(os.sched_getaffinity(0)))
         k = min(B, 32)
-        cpu = cpu_baseline((mix[:k], tgt[:k], itf[:k]), args.cpu_seconds, workers)
+        cpu = cpu_baseline((mix[:k], tgt[:k], itf[:k]), args.cpu_seconds, workers, args.workload)
 
     import torch
     import torch.distributed as dist
 
-    import avz
     from avz import metrics
     from oracle import avz_oracle as O
 
@@ -126,17 +212,11 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    plan = avz.MVDRPlan(n_fft=N_FFT, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
-                        normalize="peak", max_batch=B, max_samples=S)
-    d_mix = torch.from_numpy(mix).to(dev)
-    d_tgt = torch.from_numpy(tgt).to(dev)
-    d_itf = torch.from_numpy(itf).to(dev)
-    lens = torch.full((B,), S, dtype=torch.int32, device=dev)
-    out = plan.alloc_out(B, S, dev)
-    peak = torch.empty((B,), dtype=torch.float32, device=dev)
-
-    def step():
-        plan.run(d_mix, lens, max_len=S, ref_tgt=d_tgt, ref_int=d_itf, out=out, peak=peak)
+    if args.workload == "unet":
+        step, info = setup_unet(args, B, S, dev, mix)
+    else:
+        step, info = setup_chain(args, B, S, dev, mix, tgt, itf)
+    plan = info["plan"]
 
     for _ in range(args.warmup):
         step()
@@ -160,52 +240,72 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    chain_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     kt = plan.timing() if not args.no_kernel_timing else None
+    chain_ms = sum(kt[k] for k in plan.KERNELS) if kt else step_ms
+
+    extra = {}
+    if args.workload == "unet":  # the U-Net forward alone (features included), same items
+        bf = info["bf"]
+        items = bf.split(info["mix"])[0]
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(max(1, K // 2)):
+            bf.masks(items)
+        e1.record()
+        torch.cuda.synchronize()
+        extra["unet_ms"] = e0.elapsed_time(e1) / max(1, K // 2)
+        extra["mvdr_chain_ms"] = chain_ms
+        extra["mvdr_chain_tf_bins_per_s"] = info["bins"] / (chain_ms * 1e-3)
 
     # ---- final metrics: projection SIR per utterance (run_metrics.py:6-36), RCCL all-reduce
-    n_out = plan.out_len(S)
-    L = min(n_out, S)
-    # run_metrics.calculate_metrics_manual SIR of output and of mic 1, on the device
-    # (avz_projection_metrics), one call for both
-    est = torch.cat([out[:, :L], d_mix[:, 0, :L]])
-    m = metrics.projection_metrics(est, torch.cat([d_tgt[:, :L]] * 2),
-                                   torch.cat([d_itf[:, :L]] * 2))
+    L = S
+    if args.workload == "unet":
+        est_out = info["y"]["out"][:, :L]
+    else:
+        est_out = info["out"][:, :L]
+        L = est_out.shape[1]
+    d_mix = info["mix"]
+    d_tgt = torch.from_numpy(tgt[:, :L]).to(dev)
+    d_itf = torch.from_numpy(itf[:, :L]).to(dev)
+    est = torch.cat([est_out, d_mix[:, 0, :L]])
+    m = metrics.projection_metrics(est, torch.cat([d_tgt] * 2), torch.cat([d_itf] * 2))
     sir_out, sir_in = m[:B, 3], m[B:, 3]
     sums = torch.stack([sir_in.sum(), sir_out.sum(), torch.tensor(float(B), device=dev,
                                                                   dtype=torch.float64)])
     if world > 1:
         dist.all_reduce(sums)
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        mx = torch.tensor([chain_ms] + ([kt[k] for k in plan.KERNELS] if kt else []),
+        mx = torch.tensor([step_ms, chain_ms] + ([kt[k] for k in plan.KERNELS] if kt else []),
                           dtype=torch.float64, device=dev)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        chain_ms = float(mx[0])
+        step_ms, chain_ms = float(mx[0]), float(mx[1])
         if kt:
-            kt.update({k: float(mx[1 + j]) for j, k in enumerate(plan.KERNELS)})
+            kt.update({k: float(mx[2 + j]) for j, k in enumerate(plan.KERNELS)})
     # SIR delta vs the reference restatement on identical inputs (rank 0, few utterances)
     d_sir = None
-    if rank == 0:
+    if rank == 0 and args.workload != "unet":
         k = min(B, 4)
         got = sir_out[:k].cpu().numpy()
         refs = []
         for b in range(k):
-            r = O.oracle_debug_vec(mix[b], tgt[b], itf[b], n_fft=N_FFT, hop=HOP, sigma=1.0)
+            if args.workload == "ipd":
+                r = O.masked_mvdr_vec(mix[b], n_fft=N_FFT, hop=HOP)
+            else:
+                r = O.oracle_debug_vec(mix[b], tgt[b], itf[b], n_fft=N_FFT, hop=HOP, sigma=1.0)
             refs.append(O.projection_sdr_sir(r[:L], tgt[b, :L], itf[b, :L])[1])
         d_sir = float(np.max(np.abs(got - np.array(refs))))
 
     t_max = float(elapsed.item())
-    F, T = N_FFT // 2 + 1, -(-S // HOP) + 1
-    bins_per_rank = B * F * T
-    value = world * bins_per_rank * K / t_max
-    # Algorithmic bytes: the analysis kernel reads the 2 mic + 2 reference
-    # streams (4 x 4 B per sample = 15.97 B per TF-bin); the whole chain adds the output
-    # stream (19.96 B per TF-bin).
-    alg_analysis = B * 4 * S * 4
-    alg_chain = B * (4 * S * 4 + n_out * 4)
+    value = world * info["bins"] * K / t_max
+    # Algorithmic bytes: the analysis kernel reads the mic (+ reference)
+    # streams, 4 B per sample each (ibm: 15.97 B per TF-bin); the whole chain adds the
+    # output stream (ibm: 19.96 B per TF-bin).
+    alg_analysis, alg_chain = info["alg_analysis"], info["alg_chain"]
     traffic = {}
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
+    if os.path.exists(tf) and args.workload == "ibm":
         pm = json.load(open(tf))
         if pm.get("batch") == B and pm.get("n_fft") == N_FFT and pm.get("samples") == S:
             traffic = pm.get("hbm_bytes_per_launch", {})
@@ -217,7 +317,7 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": alg_analysis / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "traffic": traffic.get("analysis"),
-                "kernel": "avz_analysis_kernel<1024,IBM>", "kernel_ms": dom_ms,
+                "kernel": info["kernel"], "kernel_ms": dom_ms,
                 "alg_bytes_per_launch": alg_analysis,
                 "kernels_ms": {k: kt[k] for k in plan.KERNELS},
                 "chain": {"achieved": alg_chain / (chain_ms * 1e-3) / 1e9, "ms": chain_ms,
@@ -225,29 +325,39 @@ def main():
                           "frac": alg_chain / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                           "traffic": traffic.get("chain")}}
     else:
-        roof = {"bound": "hbm", "achieved": alg_chain / (chain_ms * 1e-3) / 1e9,
+        roof = {"bound": "hbm", "achieved": alg_chain / (step_ms * 1e-3) / 1e9,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": alg_chain / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "frac": alg_chain / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "traffic": traffic.get("chain"), "kernel": "avz_mvdr_batch chain",
-                "kernel_ms": chain_ms, "alg_bytes_per_launch": alg_chain}
+                "kernel_ms": step_ms, "alg_bytes_per_launch": alg_chain}
     if rank == 0:
+        cfg = {"workload": WORKLOAD_TEXT[args.workload].format(B=B, k=args.interferers),
+               "batch_per_gpu": B, "global_batch": B * world, "samples": S,
+               "n_fft": N_FFT, "hop": HOP, "parallelism":
+               f"utterance-sharded x{world}, RCCL metric all-reduce only"}
+        if args.workload == "ibm":
+            cfg.update(tf_bins_per_utt=info["bins"] // B, sigma=1.0, mask="ibm",
+                       postfilter="ibm", normalize="peak")
+        elif args.workload == "ipd":
+            cfg.update(tf_bins_per_utt=info["bins"] // B, sigma=1e-7, mask="ipd",
+                       postfilter="none", normalize="peak")
+        else:
+            cfg.update(chunk_items=info["n_items"], tf_bins_per_chunk=info["bins"] // info["n_items"],
+                       sigma=1e-5, mask="external (U-Net)", postfilter="max(M, 0.05)",
+                       normalize="none")
         line = {
             "metric": METRIC, "value": value, "unit": "TF-bins/s", "n_gpus": world,
             "steps": K, "warmup": args.warmup, "ms_per_step": 1e3 * t_max / K,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic speech-like 2-mic far-field mixtures (SURVEY 8(d)), seeds 1000+idx",
-            "config": {"workload": "configs[1]: B=256 utterances/GPU, 2 interferers, oracle IBM, "
-                                   "1024-pt STFT hop 512 @16 kHz, 4.0 s utterances",
-                       "batch_per_gpu": B, "global_batch": B * world, "samples": S,
-                       "n_fft": N_FFT, "hop": HOP, "tf_bins_per_utt": F * T, "sigma": 1.0,
-                       "mask": "ibm", "postfilter": "ibm", "normalize": "peak",
-                       "parallelism": f"utterance-sharded x{world}, RCCL metric all-reduce only"},
+            "config": cfg,
             "roofline": roof,
             "cpu_baseline": cpu,
             "sir": {"sir_in_mean_db": float(sums[0] / sums[2]),
                     "sir_out_mean_db": float(sums[1] / sums[2]),
                     "sir_abs_delta_vs_reference_db": d_sir, "n_utts": int(sums[2])},
         }
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -136,15 +136,14 @@ class NeuralMaskBeamformer:
         out, _ = self.plan.run(items, ext_mask=mask, stream=stream)
         return out
 
-    def run(self, mix: torch.Tensor, lengths=None, mask_fn=None, stream=None):
-        """mix [B, 2, S] float32 device; lengths: host sequence (default S).
-        mask_fn(items) -> [n, F, T] overrides the U-Net. Returns (y [B, S], peak [B])."""
+    def split(self, mix: torch.Tensor, lengths=None, stream=None):
+        """main_deploy's sliding windows (:137-147) of a [B, 2, S] batch as chunk items
+        [n, 2, chunk] (avz_chunk_split). Returns (items, lengths, d_len, base)."""
         B, _, S = mix.shape
         dev = mix.device
         lengths = [S] * B if lengths is None else [int(x) for x in lengths]
         utt_h, start_h, base_h = chunk_table(lengths, self.hop_c)
         n = len(utt_h)
-        st = _stream_handle(stream)
         utt = torch.from_numpy(utt_h).to(dev)
         start = torch.from_numpy(start_h).to(dev)
         base = torch.from_numpy(base_h).to(dev)
@@ -154,7 +153,16 @@ class NeuralMaskBeamformer:
                                   ct.c_void_p(start.data_ptr()), ct.c_void_p(d_len.data_ptr()),
                                   ct.c_void_p(mix.data_ptr()), mix.stride(0), mix.stride(1),
                                   ct.c_void_p(items.data_ptr()), items.stride(0), items.stride(1),
-                                  st), "avz_chunk_split")
+                                  _stream_handle(stream)), "avz_chunk_split")
+        return items, lengths, d_len, base
+
+    def run(self, mix: torch.Tensor, lengths=None, mask_fn=None, stream=None):
+        """mix [B, 2, S] float32 device; lengths: host sequence (default S).
+        mask_fn(items) -> [n, F, T] overrides the U-Net. Returns (y [B, S], peak [B])."""
+        B, _, S = mix.shape
+        dev = mix.device
+        st = _stream_handle(stream)
+        items, lengths, d_len, base = self.split(mix, lengths, stream)
         mask = mask_fn(items) if mask_fn is not None else self.masks(items)
         item_out = self.beamform(items, mask, stream=stream)
         y = torch.zeros((B, S), dtype=torch.float32, device=dev)
