@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "avz_common.hpp"
@@ -128,18 +129,15 @@ __device__ __forceinline__ float irm_gain(cf zr, cf zrp) {
 
 // ================================ analysis ================================
 template <int N, int MASK>
-__global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A) {
+__device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char* lds, int c,
+                                              int b) {
   using C = KCfg<N>;
   using G = CGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
   constexpr int FB = (MASK == MASK_IBM) ? NSLOT / 2 : NSLOT;  // frames per step
   static_assert(kChunk % FB == 0, "steps tile the chunk");
 
-  extern __shared__ __align__(16) unsigned char lds[];
   cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
-  C::Fft::fill_twiddles(twid, threadIdx.x, NT);
-
-  const int c = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
@@ -322,7 +320,20 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A)
       if constexpr (MASK == MASK_IBM) MW[N / 2] = nyq_bits;
     }
   }
+}
 
+// Persistent grid (about two blocks per CU): block i takes the (chunk, utterance) items
+// i, i + gridDim.x, ... so the twiddle table is built once per block and the batch is
+// spread evenly over the resident blocks (no second, partly idle round of short blocks).
+template <int N, int MASK>
+__global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A) {
+  using G = CGeo<N>;
+  extern __shared__ __align__(16) unsigned char lds[];
+  KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
+  const int gx = (A.max_frames + kChunk - 1) / kChunk;
+  const int n_items = gx * A.batch;
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x)
+    analysis_item<N, MASK>(A, lds, it % gx, it / gx);
 }
 
 // ================================ solve ================================
@@ -428,7 +439,8 @@ __global__ void __launch_bounds__(kSrpThreads) avz_srp_kernel(ChainArgs A, SrpAr
 
 // ================================ synthesis ================================
 template <int N, int PF>
-__global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(ChainArgs A) {
+__device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char* lds, int c,
+                                               int b) {
   using C = KCfg<N>;
   using G = CGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
@@ -439,12 +451,8 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(ChainArgs A
   constexpr int SPT = FB / NSG;       // segments per thread per step
   static_assert(SPT * NSG == FB, "OLA mapping");
 
-  extern __shared__ __align__(16) unsigned char lds[];
   cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
   float* red = reinterpret_cast<float*>(lds + G::MISC_OFF);
-  C::Fft::fill_twiddles(twid, threadIdx.x, NT);
-
-  const int c = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
@@ -681,6 +689,18 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(ChainArgs A
   AVZ_STAMP(10);
 }
 
+// Persistent grid over (chunk, utterance) items, as avz_analysis_kernel.
+template <int N, int PF>
+__global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(ChainArgs A) {
+  using G = CGeo<N>;
+  extern __shared__ __align__(16) unsigned char lds[];
+  KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
+  const int gx = (A.max_frames + kChunk - 1) / kChunk;
+  const int n_items = gx * A.batch;
+  for (int it = blockIdx.x; it < n_items; it += gridDim.x)
+    synthesis_item<N, PF>(A, lds, it % gx, it / gx);
+}
+
 // ================================ finalize ================================
 template <int N>
 __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
@@ -742,6 +762,20 @@ extern "C" int avz_debug_set_stamps_chunked(void* dev_ptr) {
 }
 #endif
 
+// Compute units of the current device (cached per process; one device per process here).
+static int resident_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
 template <typename K>
 static bool set_lds(K kern, int lds) {
   return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) ==
@@ -763,6 +797,8 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
   const dim3 grid(nch, a->batch);
+  const int n_items = nch * a->batch;
+  const dim3 pgrid((unsigned)std::min(n_items, 2 * resident_cus()));  // ~2 blocks per CU
   constexpr int F = N / 2 + 1;
   const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
   hipEvent_t const* ev = reinterpret_cast<hipEvent_t const*>(a->events);
@@ -770,11 +806,11 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
     if (ev) (void)hipEventRecord(ev[i], st);
   };
   mark(0);
-  hipLaunchKernelGGL(k1, grid, dim3(kCThreads), lds, st, *a);
+  hipLaunchKernelGGL(k1, pgrid, dim3(kCThreads), lds, st, *a);
   mark(1);
   hipLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, *a);
   mark(2);
-  hipLaunchKernelGGL(k2, grid, dim3(kCThreads), lds, st, *a);
+  hipLaunchKernelGGL(k2, pgrid, dim3(kCThreads), lds, st, *a);
   mark(3);
   hipLaunchKernelGGL(k3, grid, dim3(kCThreads), 0, st, *a);
   mark(4);
@@ -806,7 +842,9 @@ static int launch_srp_t(const ChainArgs* a, const SrpArgs* s, hipStream_t st) {
   }
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
-  hipLaunchKernelGGL(k1, dim3(nch, a->batch), dim3(kCThreads), lds, st, *a);
+  const int n_items = nch * a->batch;
+  hipLaunchKernelGGL(k1, dim3((unsigned)std::min(n_items, 2 * resident_cus())), dim3(kCThreads),
+                     lds, st, *a);
   hipLaunchKernelGGL(avz_srp_kernel<N>, dim3(a->batch), dim3(kSrpThreads), 0, st, *a, *s);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -52,6 +52,57 @@ __global__ void __launch_bounds__(NT, 1) bench_x1(const float* in, float* out, i
   out[blockIdx.x * NT + threadIdx.x] = acc;
 }
 
+
+// MODE 0: FFT only (its own transpose; no spectrum round trip, no block barrier)
+// MODE 1: FFT + register-resident partner fetch (ds_bpermute) + cross-half swaps
+// MODE 2: FFT + spectrum store/reload through LDS, wave-local (no block barrier)
+template <int NT, int MODE>
+__global__ void __launch_bounds__(NT, 2) bench_x2m(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 5, l = lane & 31;
+  cf* tw = reinterpret_cast<cf*>(lds + (NT / 64) * 16896);
+  Fft1024x2::fill_twiddles(tw, threadIdx.x, NT);
+  Fft1024x2 f; f.init(lane);
+  cf* scr = reinterpret_cast<cf*>(lds + wave * 16896 + g * 8448);
+  cf v[32];
+  static_for<0, 32>([&](auto r) { v[r] = {in[(l + 32 * r) & 1023], in[(l + 32 * r + 7) & 1023]}; });
+  __syncthreads();
+  const int paddr = 4 * (g * 32 + ((32 - l) & 31));
+  float acc = 0;
+  for (int it = 0; it < iters; ++it) {
+    f.forward(v, scr, tw);
+    if constexpr (MODE == 1) {
+      cf P[16];
+      static_for<0, 16>([&](auto k) {
+        cf s = v[31 - k];
+        cf q = {__int_as_float(__builtin_amdgcn_ds_bpermute(paddr, __float_as_int(s.x))),
+                __int_as_float(__builtin_amdgcn_ds_bpermute(paddr, __float_as_int(s.y)))};
+        const cf own = v[(32 - k) & 31];
+        P[k] = (l == 0) ? own : q;
+      });
+      static_for<0, 8>([&](auto k) {
+        auto sw = [&](float& a, float& b) {
+          auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+          a = __uint_as_float(r[0]); b = __uint_as_float(r[1]);
+        };
+        sw(v[k].x, v[k + 8].x); sw(v[k].y, v[k + 8].y);
+        sw(P[k].x, P[k + 8].x); sw(P[k].y, P[k + 8].y);
+      });
+      // consume like the bin phase would (2 bins worth of products per k)
+      static_for<0, 8>([&](auto k) {
+        acc += v[k].x * P[k].x + v[k].y * P[k].y + v[k + 8].x * P[k + 8].y - v[k + 8].y * P[k + 8].x;
+      });
+    } else if constexpr (MODE == 2) {
+      static_for<0, 32>([&](auto k) { scr[l + 32 * k] = v[k]; });
+      __builtin_amdgcn_wave_barrier();
+      static_for<0, 32>([&](auto k) { v[k] = scr[(l * 33 + k) & 1023]; });
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  static_for<0, 32>([&](auto k) { acc += v[k].x + v[k].y; });
+  out[blockIdx.x * NT + threadIdx.x] = acc;
+}
+
 extern "C" int run_bench(int variant, const float* in, float* out, int blocks, int iters) {
   switch (variant) {
     case 0: { auto k = bench_x2<512>; int lds = 8 * 16896 + 8192;
@@ -64,6 +115,10 @@ extern "C" int run_bench(int variant, const float* in, float* out, int blocks, i
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, 0, in, out, iters); break; }
     case 3: { auto k = bench_x2<256>; int lds = 4 * 16896 + 8192;
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
+    case 4: case 5: case 6: { auto k = variant == 4 ? bench_x2m<256, 0> : variant == 5 ? bench_x2m<256, 1> : bench_x2m<256, 2>;
+      int lds = 4 * 16896 + 8192;
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
   }
