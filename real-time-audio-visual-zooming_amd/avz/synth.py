@@ -81,6 +81,73 @@ def make_scene(idx: int, n_samples: int = 64000, n_interferers: int = 1, d: floa
             (int_m[0] / peak).astype(np.float32))
 
 
+def write_world_scene(out_dir: str, mix: np.ndarray, tgt: np.ndarray, itf: np.ndarray,
+                      fs: int = FS) -> str:
+    """rt_av_zoom/core/world.py:236-263 on-disk format (what oracle_debug.py:35-39 and
+    masked_mvdr.py read): stereo ``mixture.wav`` [S, 2] and the mic-1 references as mono
+    ``target_reference.wav`` / ``interference_reference.wav``, each reference peak-normalised
+    on its own (world.py:243-244). 16-bit PCM like soundfile's WAV default."""
+    import os
+
+    from . import wavio
+    os.makedirs(out_dir, exist_ok=True)
+    wavio.write(os.path.join(out_dir, "mixture.wav"), np.asarray(mix).T, fs)
+    for name, r in (("target_reference.wav", tgt), ("interference_reference.wav", itf)):
+        r = np.asarray(r, np.float64)
+        wavio.write(os.path.join(out_dir, name), r / (np.max(np.abs(r)) + 1e-9), fs)
+    return out_dir
+
+
+def write_final_pipeline_scene(save_dir: str, mix: np.ndarray, tgt: np.ndarray,
+                               itf: np.ndarray, tgt2: np.ndarray | None = None,
+                               itf2: np.ndarray | None = None, fs: int = FS) -> str:
+    """Final_pipeline/src/simulation.py:191-211 format (what run.py inf / eval read):
+    stereo ``mixture.wav``, ``target.wav`` and ``interference.wav``, all divided by the
+    mixture's peak (the arrays here are already on that shared scale, make_scene).
+    ``tgt2``/``itf2`` are the mic-2 images (default: the mic-1 ones). Returns mixture.wav."""
+    import os
+
+    from . import wavio
+    os.makedirs(save_dir, exist_ok=True)
+    tgt2 = tgt if tgt2 is None else tgt2
+    itf2 = itf if itf2 is None else itf2
+    wavio.write(os.path.join(save_dir, "mixture.wav"), np.asarray(mix).T, fs)
+    wavio.write(os.path.join(save_dir, "target.wav"), np.stack([tgt, tgt2], axis=1), fs)
+    wavio.write(os.path.join(save_dir, "interference.wav"), np.stack([itf, itf2], axis=1), fs)
+    return os.path.join(save_dir, "mixture.wav")
+
+
+def mix_and_save(sources, prefix: str, angles=(90.0, 40.0, 130.0), d: float = 0.04,
+                 fs: int = FS, out_dir: str = "."):
+    """full_audio_generating_pipeline/world_building.py:68-100 for given mono sources
+    (target first): far-field fractional delays per mic, mic-1 target / interference
+    references, shared peak normalisation; writes mixture_<prefix>.wav (stereo),
+    target_ref_<prefix>.wav, interf_ref_<prefix>.wav. Returns (mix [2, S], tgt, itf)."""
+    import os
+
+    from . import wavio
+    n = max(len(s) for s in sources)
+    # sources keep their dtype: the reference loads float32 (world_building.py:62), so its
+    # forward rfft runs in single precision (numpy >= 2)
+    raws = [np.pad(np.asarray(s), (0, n - len(s))) for s in sources]
+    m1, m2, tgt_ref, int_ref = (np.zeros(n) for _ in range(4))
+    for i, (r, a) in enumerate(zip(raws, angles)):
+        t1, t2 = far_field_delays(a, d)
+        s1 = frac_delay(r, t1, fs)
+        m1 += s1
+        m2 += frac_delay(r, t2, fs)
+        if i == 0:
+            tgt_ref += s1
+        else:
+            int_ref += s1
+    mix = np.stack([m1, m2])
+    norm = np.max(np.abs(mix)) + 1e-9
+    wavio.write(os.path.join(out_dir, f"mixture_{prefix}.wav"), (mix / norm).T, fs)
+    wavio.write(os.path.join(out_dir, f"target_ref_{prefix}.wav"), tgt_ref / norm, fs)
+    wavio.write(os.path.join(out_dir, f"interf_ref_{prefix}.wav"), int_ref / norm, fs)
+    return mix / norm, tgt_ref / norm, int_ref / norm
+
+
 def make_batch(batch: int, start: int = 0, n_samples: int = 64000, n_interferers: int = 2,
                **kw):
     """[B, 2, S] mix, [B, S] target ref, [B, S] interference ref (float32)."""

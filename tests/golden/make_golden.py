@@ -19,7 +19,7 @@ Final_pipeline/src/inference.py imports tensorflow at module level; an empty sta
 module is injected (only TFLiteBeamformer uses it, and that class is replaced by
 _MaskFeeder below because the .tflite model file is absent).
 
-Usage:  python tests/golden/make_golden.py [hybrid] [srp] [report] [reverb] [neural]
+Usage:  python tests/golden/make_golden.py [hybrid] [srp] [report] [reverb] [neural] [world]
         (writes tests/golden/*.npz)
 """
 from __future__ import annotations
@@ -414,6 +414,36 @@ def gen_neural(trip, run_metrics, save):
             os.chdir(cwd)
 
 
+def gen_world(trip, save):
+    """full_audio_generating_pipeline/world_building.py mix_and_save (:68-100) on three
+    1.5-s mono excerpts of the bundled references (target first). kagglehub and librosa
+    are imported at module level but not used on this path (the WAVs are already 16 kHz,
+    so load_resample never resamples): empty stand-ins are injected."""
+    import importlib
+    for name in ("kagglehub", "librosa"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    wb = importlib.import_module("rt_av_zoom.core.full_audio_generating_pipeline.world_building")
+    seg = slice(40000, 48000)
+    srcs = [trip["test"][1][seg], trip["test"][2][seg], trip["set2"][1][seg]]
+    with tempfile.TemporaryDirectory() as td:
+        files = []
+        for j, s in enumerate(srcs):
+            files.append(os.path.join(td, f"src{j}.wav"))
+            wavfile.write(files[-1], 16000, s)
+        cwd = os.getcwd()
+        os.chdir(td)
+        _WRITES.clear()
+        try:
+            with contextlib.redirect_stdout(open(os.devnull, "w")):
+                wb.mix_and_save(files, "golden")
+        finally:
+            os.chdir(cwd)
+    save("world_mix.npz", sources=np.stack(srcs), d=wb.D,
+         angles=np.array([wb.ANGLE_TARGET, wb.ANGLE_INTERFERER_A, wb.ANGLE_INTERFERER_B]),
+         mixture=_WRITES["mixture_golden.wav"], target_ref=_WRITES["target_ref_golden.wav"],
+         interf_ref=_WRITES["interf_ref_golden.wav"])
+
+
 def gen_report(trip, metrics, save):
     """Final_pipeline/src/metrics.py evaluate_run on a simulated-run folder built from the
     test triple (stereo target/interference/mixture as simulation.py:205-211 writes them)
@@ -470,6 +500,8 @@ def main():
             gen_reverb(trip, run_metrics, save)
         if "neural" in only:
             gen_neural(trip, run_metrics, save)
+        if "world" in only:
+            gen_world(trip, save)
         with open(mpath, "w") as fh:
             json.dump(manifest, fh, indent=1, sort_keys=True)
         return
@@ -557,6 +589,7 @@ def main():
     gen_report(trip, metrics, save)
     gen_reverb(trip, run_metrics, save)
     gen_neural(trip, run_metrics, save)
+    gen_world(trip, save)
 
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)
