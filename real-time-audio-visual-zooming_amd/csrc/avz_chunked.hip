@@ -128,7 +128,7 @@ __device__ __forceinline__ float irm_gain(cf zr, cf zrp) {
 }
 
 // ================================ analysis ================================
-template <int N, int MASK>
+template <int N, int MASK, bool IRM>
 __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char* lds, int c,
                                               int b) {
   using C = KCfg<N>;
@@ -195,10 +195,9 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     acc[j].zero();
     bits[j] = 0u;
   }
-  // IRM post-filter gains of this chunk (PF_IRM plans only; block-uniform)
-  float* const gain = (MASK == MASK_IBM && A.pf_gain)
-                          ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F
-                          : nullptr;
+  // IRM post-filter gains of this chunk (PF_IRM plans only)
+  static_assert(!IRM || MASK == MASK_IBM, "IRM needs the references");
+  float* const gain = IRM ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F : nullptr;
   // Nyquist bin N/2: frame `lane` of each step on the last wave's lanes.
   const bool nyq_wave = (wave == G::NWAVE - 1);
   Acc32 an;
@@ -257,9 +256,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
                   bin_mask<MASK>(A, b, x0, x1, zr[i], zrp[i], kb, f0 + g0 + i, noise, wgt);
               bits[j] |= (noise ? 1u : 0u) << (step * FB + g0 + i);
               acc[j].add(x0, x1, wgt, m);
-              if constexpr (MASK == MASK_IBM) {
-                if (gain) gain[(step * FB + g0 + i) * F + kb] = irm_gain(zr[i], zrp[i]);
-              }
+              if constexpr (IRM) gain[(step * FB + g0 + i) * F + kb] = irm_gain(zr[i], zrp[i]);
             }
           }
         }
@@ -279,9 +276,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         float wn;
         const float mn = bin_mask<MASK>(A, b, y0, y1, zr, zr, N / 2, f0 + lane, noise, wn);
         an.add(y0, y1, wn, mn);
-        if constexpr (MASK == MASK_IBM) {
-          if (gain) gain[(step * FB + lane) * F + N / 2] = irm_gain(zr, zr);
-        }
+        if constexpr (IRM) gain[(step * FB + lane) * F + N / 2] = irm_gain(zr, zr);
       }
       const unsigned long long bal = __ballot(noise);
       nyq_bits |= ((uint32_t)bal & ((1u << FB) - 1u)) << (step * FB);
@@ -325,7 +320,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
 // Persistent grid (about two blocks per CU): block i takes the (chunk, utterance) items
 // i, i + gridDim.x, ... so the twiddle table is built once per block and the batch is
 // spread evenly over the resident blocks (no second, partly idle round of short blocks).
-template <int N, int MASK>
+template <int N, int MASK, bool IRM>
 __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A) {
   using G = CGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -333,7 +328,7 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A)
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
   const int n_items = gx * A.batch;
   for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-    analysis_item<N, MASK>(A, lds, it % gx, it / gx);
+    analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx);
 }
 
 // ================================ solve ================================
@@ -784,7 +779,7 @@ static bool set_lds(K kern, int lds) {
 
 template <int N, int MASK, int PF>
 static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
-  auto k1 = avz_analysis_kernel<N, MASK>;
+  auto k1 = avz_analysis_kernel<N, MASK, PF == PF_IRM>;
   auto k2 = avz_synthesis_kernel<N, PF>;
   auto k3 = avz_finalize_kernel<N>;
   auto ks = avz_solve_kernel<N>;
@@ -833,7 +828,7 @@ static int launch_pf(const ChainArgs* a, hipStream_t st) {
 
 template <int N>
 static int launch_srp_t(const ChainArgs* a, const SrpArgs* s, hipStream_t st) {
-  auto k1 = avz_analysis_kernel<N, MASK_ONES>;
+  auto k1 = avz_analysis_kernel<N, MASK_ONES, false>;
   constexpr int lds = CGeo<N>::LDS_BYTES;
   static bool attr_done = false;
   if (!attr_done) {
