@@ -67,6 +67,8 @@ def parse():
                     help="time box of the CPU baseline workers")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, available cores)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--rehearse-shared-gpu", action="store_true",
+                    help="N > 1 rehearsal on one GPU: all ranks on cuda:0, gloo collectives")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-kernel HIP events (roofline from the step events)")
     a = ap.parse_args()
@@ -207,10 +209,16 @@ def main():
     from avz import metrics
     from oracle import avz_oracle as O
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # --rehearse-shared-gpu: every rank on cuda:0 with gloo, to exercise the N > 1 code
+    # path (sharding, metric all-reduce, max-over-ranks timing) on a one-GPU box
+    gpu = 0 if args.rehearse_shared_gpu else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse_shared_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     if args.workload == "unet":
         step, info = setup_unet(args, B, S, dev, mix)
