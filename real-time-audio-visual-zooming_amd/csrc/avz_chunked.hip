@@ -76,6 +76,19 @@ __device__ __forceinline__ float inv_wsum(int m) {
   return 1.0f / (wa * wa + wb * wb);
 }
 
+// Window + forward FFT with the lane's twiddles in registers (N = 1024 analysis).
+__device__ __forceinline__ void window_fft_reg(cf (&v)[32], const WinCoef<1024>& wc,
+                                               const Fft1024x2& fft, cf* spec,
+                                               const cf (&tw_reg)[31], const LaneMap<1024>& lm) {
+  static_for<0, 32>([&](auto r) {
+    constexpr float cr = W32::c[r], sr = -W32::s[r];
+    const float w = fmaf(wc.as, sr, fmaf(-wc.ac, cr, wc.a0));
+    v[r] = c_scale(v[r], w);
+  });
+  fft.forward_reg(v, spec, tw_reg);
+  static_for<0, 32>([&](auto k) { spec[lm.out0 + 32 * k] = v[k]; });
+}
+
 template <int N>
 __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<N>& wc,
                                            const typename KCfg<N>::Fft& fft, cf* spec,
@@ -128,9 +141,10 @@ __device__ __forceinline__ float irm_gain(cf zr, cf zrp) {
 }
 
 // ================================ analysis ================================
-template <int N, int MASK, bool IRM>
+struct NoTw {};
+template <int N, int MASK, bool IRM, class TW>
 __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char* lds, int c,
-                                              int b) {
+                                              int b, const TW& tw_reg) {
   using C = KCfg<N>;
   using G = CGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
@@ -215,7 +229,12 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     AVZ_STAMP(0);
 #endif
-    if (live) window_fft<N>(v, wc, fft, my_spec, twid, lm);
+    if (live) {
+      if constexpr (std::is_same<TW, NoTw>::value)
+        window_fft<N>(v, wc, fft, my_spec, twid, lm);
+      else
+        window_fft_reg(v, wc, fft, my_spec, tw_reg, lm);
+    }
     if (step + 1 < nstep) issue_loads(step + 1);
     lds_barrier();
     AVZ_STAMP(1);
@@ -327,8 +346,18 @@ __global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A)
   KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
   const int n_items = gx * A.batch;
-  for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-    analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx);
+  if constexpr (N == 1024) {
+    __syncthreads();
+    cf tw_reg[31];
+    Fft1024x2 f;
+    f.init(threadIdx.x & 63);
+    f.load_twiddles(tw_reg, reinterpret_cast<const cf*>(lds + G::TW_OFF));
+    for (int it = blockIdx.x; it < n_items; it += gridDim.x)
+      analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, tw_reg);
+  } else {
+    for (int it = blockIdx.x; it < n_items; it += gridDim.x)
+      analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, NoTw{});
+  }
 }
 
 // ================================ solve ================================

@@ -281,6 +281,21 @@ struct Fft1024x2 {
       }
     });
   }
+  // stage1 with the lane's 31 twiddles W1024^{l k1} (k1 = 1..31) held in registers
+  // (tw_reg[k1 - 1]); for kernels with VGPRs to spare, saves 32 LDS reads per FFT pair.
+  __device__ __forceinline__ void stage1_reg(cf (&v)[32], const cf (&tw_reg)[31]) const {
+    dft32(v);
+    static_for<1, 32>([&](auto k) { v[k] = c_mul(v[k], tw_reg[k - 1]); });
+  }
+  __device__ __forceinline__ void load_twiddles(cf (&tw_reg)[31], const cf* tw) const {
+    static_for<1, 32>([&](auto k) { tw_reg[k - 1] = tw[k * 32 + l]; });
+  }
+  __device__ __forceinline__ void forward_reg(cf (&v)[32], cf* scratch,
+                                              const cf (&tw_reg)[31]) const {
+    stage1_reg(v, tw_reg);
+    transpose(v, scratch);
+    stage2(v);
+  }
   __device__ __forceinline__ void transpose(cf (&v)[32], cf* scratch) const {
     static_for<0, 32>([&](auto k) { scratch[k * 33 + l] = v[k]; });
     __builtin_amdgcn_wave_barrier();

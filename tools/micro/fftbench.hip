@@ -70,7 +70,18 @@ __global__ void __launch_bounds__(NT, 2) bench_x2m(const float* in, float* out, 
   const int paddr = 4 * (g * 32 + ((32 - l) & 31));
   float acc = 0;
   for (int it = 0; it < iters; ++it) {
-    f.forward(v, scr, tw);
+    if constexpr (MODE == 3) {
+      f.stage1(v, tw);
+      __builtin_amdgcn_sched_barrier(0);
+      f.stage2(v);
+    } else if constexpr (MODE == 4) {
+      static_for<0, 32>([&](auto k) { v[k] = c_mul(v[k], cf{0.70710678f, -0.70710678f}); });
+      dft32(v);
+      __builtin_amdgcn_sched_barrier(0);
+      dft32(v);
+    } else {
+      f.forward(v, scr, tw);
+    }
     if constexpr (MODE == 1) {
       cf P[16];
       static_for<0, 16>([&](auto k) {
@@ -92,6 +103,9 @@ __global__ void __launch_bounds__(NT, 2) bench_x2m(const float* in, float* out, 
       static_for<0, 8>([&](auto k) {
         acc += v[k].x * P[k].x + v[k].y * P[k].y + v[k + 8].x * P[k + 8].y - v[k + 8].y * P[k + 8].x;
       });
+    } else if constexpr (MODE == 3 || MODE == 4) {
+      // (timing only) the FFT's arithmetic without its LDS transpose; MODE 4 also
+      // without the LDS twiddle reads
     } else if constexpr (MODE == 2) {
       static_for<0, 32>([&](auto k) { scr[l + 32 * k] = v[k]; });
       __builtin_amdgcn_wave_barrier();
@@ -117,7 +131,7 @@ extern "C" int run_bench(int variant, const float* in, float* out, int blocks, i
     case 3: { auto k = bench_x2<256>; int lds = 4 * 16896 + 8192;
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
-    case 4: case 5: case 6: { auto k = variant == 4 ? bench_x2m<256, 0> : variant == 5 ? bench_x2m<256, 1> : bench_x2m<256, 2>;
+    case 4: case 5: case 6: case 7: case 8: { auto k = variant == 4 ? bench_x2m<256, 0> : variant == 5 ? bench_x2m<256, 1> : variant == 6 ? bench_x2m<256, 2> : variant == 7 ? bench_x2m<256, 3> : bench_x2m<256, 4>;
       int lds = 4 * 16896 + 8192;
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
