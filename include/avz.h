@@ -192,6 +192,24 @@ int avz_projection_metrics(int batch, int max_len, const int* len, const float* 
                            const float* itf, long long itf_stride, double* sums,
                            double* metrics, void* hip_stream);
 
+/* Synthetic scene mixing on the device — the anechoic far-field generator of
+ * full_audio_generating_pipeline/world_building.py:47-59 (per-mic fractional delay by an
+ * rfft phase shift over the whole signal, d = mic_d, c = c_sound) with the SIR gain
+ * (Final_pipeline/src/simulation.py:167-179, on mic 1), AWGN at snr_db per channel
+ * (world.py:93-98, noise = sqrt(mean(clean^2)/10^(snr/10)) * z) and the shared peak
+ * normalisation of simulation.py:197-202 (peak = max|mix| + 1e-9).
+ * src[b][s][0..n) are the mono sources (s = 0 the target, 1..n_src-1 interferers) at
+ * angles_deg[b][s]; noise[b][c][0..n) unit-normal draws for mic c. Writes
+ * mix[b][c] (at mix_stride / ch_stride), tgt[b] = mic-1 target image / peak,
+ * itf[b] = mic-1 interference image / peak. `workspace` holds
+ * avz_scene_workspace_bytes(batch, n_src, n) bytes. All arrays device-resident. */
+long long avz_scene_workspace_bytes(int batch, int n_src, int n);
+int avz_scene_mix(int batch, int n_src, int n, const float* src, const double* angles_deg,
+                  const float* noise, double mic_d, double c_sound, double fs, double sir_db,
+                  double snr_db, float* mix, long long mix_stride, long long ch_stride,
+                  float* tgt, float* itf, long long ref_stride, void* workspace,
+                  long long workspace_bytes, void* hip_stream);
+
 const char* avz_strerror(int code);
 /* Last HIP error string recorded by the library on this thread (diagnostics). */
 const char* avz_last_hip_error(void);

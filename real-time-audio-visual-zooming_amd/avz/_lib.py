@@ -35,7 +35,7 @@ EXPORTED = [
     "avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
     "avz_mvdr_batch", "avz_plan_set_timing", "avz_plan_get_timing", "avz_stft",
     "avz_chunk_split", "avz_chunk_merge", "avz_mask_features", "avz_srp_scan",
-    "avz_projection_metrics", "avz_strerror",
+    "avz_projection_metrics", "avz_scene_workspace_bytes", "avz_scene_mix", "avz_strerror",
     "avz_last_hip_error", "avz_version",
 ]
 
@@ -108,13 +108,16 @@ def _load():
     D = ct.c_double
     lib.avz_srp_scan.argtypes = [P, I, P, I, P, LL, LL, I, D, D, D, D, P, P]
     lib.avz_projection_metrics.argtypes = [I, I, P, P, LL, P, LL, P, LL, P, P, P]
+    lib.avz_scene_workspace_bytes.argtypes = [I, I, I]
+    lib.avz_scene_workspace_bytes.restype = LL
+    lib.avz_scene_mix.argtypes = [I, I, I, P, P, P, D, D, D, D, D, P, LL, LL, P, P, LL, P, LL, P]
     lib.avz_strerror.argtypes = [ct.c_int]
     lib.avz_strerror.restype = ct.c_char_p
     lib.avz_last_hip_error.restype = ct.c_char_p
     for name in ("avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
                  "avz_mvdr_batch", "avz_stft", "avz_chunk_split", "avz_chunk_merge",
                  "avz_plan_set_timing", "avz_plan_get_timing", "avz_mask_features",
-                 "avz_srp_scan", "avz_projection_metrics",
+                 "avz_srp_scan", "avz_projection_metrics", "avz_scene_mix",
                  "avz_version"):
         getattr(lib, name).restype = ct.c_int
     return lib

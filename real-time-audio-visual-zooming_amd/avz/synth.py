@@ -148,6 +148,54 @@ def mix_and_save(sources, prefix: str, angles=(90.0, 40.0, 130.0), d: float = 0.
     return mix / norm, tgt_ref / norm, int_ref / norm
 
 
+def scene_draws(idx: int, n_samples: int = 64000, n_interferers: int = 1, fs: int = FS):
+    """The random draws of make_scene(idx) in its RNG order: angles [1 + K] (target 90
+    deg first), sources [1 + K, S] and the unit-normal AWGN draws [2, S] (rng.normal(0, s)
+    is s * standard_normal in numpy's Generator, so the device scales these)."""
+    rng = np.random.default_rng(1000 + idx)
+    angles = [40.0] + list(rng.uniform(0.0, 180.0, max(0, n_interferers - 1)))
+    srcs = [speech_like(rng, n_samples, fs)]
+    for _ in angles[:n_interferers]:
+        srcs.append(speech_like(rng, n_samples, fs))
+    z = np.stack([rng.standard_normal(n_samples), rng.standard_normal(n_samples)])
+    return np.array([90.0] + angles[:n_interferers]), np.stack(srcs), z
+
+
+def make_batch_device(batch: int, start: int = 0, n_samples: int = 64000,
+                      n_interferers: int = 2, d: float = MIC_D, sir_db: float = 0.0,
+                      snr_db: float = 5.0, fs: int = FS, device=None):
+    """make_batch on the device: the host draws the sources and noise (same RNG stream
+    as make_scene), avz_scene_mix does the fractional delays, SIR gain, AWGN and peak
+    normalisation. Returns device tensors (mix [B, 2, S], tgt [B, S], itf [B, S])."""
+    import ctypes as ct
+
+    import torch
+
+    from ._lib import check, lib
+    from .engine import _stream_handle
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    K = n_interferers
+    angles = np.empty((batch, 1 + K))
+    srcs = np.empty((batch, 1 + K, n_samples), np.float32)
+    noise = np.empty((batch, 2, n_samples), np.float32)
+    for b in range(batch):
+        angles[b], srcs[b], noise[b] = scene_draws(start + b, n_samples, K, fs)
+    d_ang = torch.from_numpy(angles).to(dev)
+    d_src = torch.from_numpy(srcs).to(dev)
+    d_noise = torch.from_numpy(noise).to(dev)
+    mix = torch.empty((batch, 2, n_samples), dtype=torch.float32, device=dev)
+    tgt = torch.empty((batch, n_samples), dtype=torch.float32, device=dev)
+    itf = torch.empty((batch, n_samples), dtype=torch.float32, device=dev)
+    ws_bytes = lib.avz_scene_workspace_bytes(batch, 1 + K, n_samples)
+    ws = torch.empty((max(ws_bytes, 4) + 3) // 4, dtype=torch.float32, device=dev)
+    p = lambda t: ct.c_void_p(t.data_ptr())  # noqa: E731
+    check(lib.avz_scene_mix(batch, 1 + K, n_samples, p(d_src), p(d_ang), p(d_noise), d, C_SOUND,
+                            float(fs), sir_db, snr_db, p(mix), mix.stride(0), mix.stride(1),
+                            p(tgt), p(itf), tgt.stride(0), p(ws), ws_bytes,
+                            _stream_handle(None)), "avz_scene_mix")
+    return mix, tgt, itf
+
+
 def make_batch(batch: int, start: int = 0, n_samples: int = 64000, n_interferers: int = 2,
                **kw):
     """[B, 2, S] mix, [B, S] target ref, [B, S] interference ref (float32)."""

@@ -447,6 +447,51 @@ extern "C" int avz_srp_scan(const avz_plan* p, int batch, const int* len, int ma
   return rc;
 }
 
+extern "C" long long avz_scene_workspace_bytes(int batch, int n_src, int n) {
+  if (batch <= 0 || n_src <= 0 || n <= 0) return 0;
+  return 2LL * batch * n_src * 2 * n * (long long)sizeof(float);
+}
+
+extern "C" int avz_scene_mix(int batch, int n_src, int n, const float* src,
+                             const double* angles_deg, const float* noise, double mic_d,
+                             double c_sound, double fs, double sir_db, double snr_db, float* mix,
+                             long long mix_stride, long long ch_stride, float* tgt, float* itf,
+                             long long ref_stride, void* workspace, long long workspace_bytes,
+                             void* stream) {
+  if (batch < 0 || n_src < 1 || n < 2 || (n & 1)) return AVZ_ERR_SHAPE;  // irfft pairs: n even
+  if (batch == 0) return AVZ_OK;
+  if (!src || !angles_deg || !noise || !mix || !tgt || !itf || !workspace) return AVZ_ERR_ARG;
+  if (!(fs > 0) || !(c_sound > 0)) return AVZ_ERR_ARG;
+  if (ch_stride < n || (batch > 1 && (mix_stride < ch_stride + n || ref_stride < n)))
+    return AVZ_ERR_SHAPE;
+  if (workspace_bytes < avz_scene_workspace_bytes(batch, n_src, n)) return AVZ_ERR_SHAPE;
+  if ((long long)batch * n_src * 2 > 65535) return AVZ_ERR_UNSUPPORTED;  // grid.y
+  avz::SceneArgs s{};
+  s.batch = batch;
+  s.n_src = n_src;
+  s.n = n;
+  s.src = src;
+  s.angles_deg = angles_deg;
+  s.noise = noise;
+  s.mic_d = mic_d;
+  s.c_sound = c_sound;
+  s.fs = fs;
+  s.sir_db = sir_db;
+  s.snr_db = snr_db;
+  const long long per = (long long)batch * n_src * 2 * n;
+  s.hk = static_cast<float*>(workspace);
+  s.img = s.hk + per;
+  s.mix = mix;
+  s.mix_stride = mix_stride;
+  s.ch_stride = ch_stride;
+  s.tgt = tgt;
+  s.itf = itf;
+  s.ref_stride = ref_stride;
+  const int rc = avz_launch_scene(&s, stream);
+  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  return rc;
+}
+
 extern "C" int avz_projection_metrics(int batch, int max_len, const int* len, const float* est,
                                       long long est_stride, const float* tgt,
                                       long long tgt_stride, const float* itf,

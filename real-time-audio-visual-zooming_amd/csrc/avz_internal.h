@@ -104,9 +104,25 @@ struct ChunkMergeArgs {
   float norm_eps;
 };
 
+struct SceneArgs {
+  int batch, n_src, n;        // utterances, sources per utterance (target first), samples
+  const float* src;           // [B][n_src][n]
+  const double* angles_deg;   // [B][n_src] azimuths
+  const float* noise;         // [B][2][n] unit-normal AWGN draws
+  double mic_d, c_sound, fs, sir_db, snr_db;
+  float* hk;                  // workspace [B][n_src][2][n] fractional-delay kernels
+  float* img;                 // workspace [B][n_src][2][n] per-mic source images
+  float* mix;                 // [B][mix_stride]: mic channels at ch_stride
+  long long mix_stride, ch_stride;
+  float* tgt;                 // [B][ref_stride] mic-1 target image / peak
+  float* itf;                 // [B][ref_stride] mic-1 interference image / peak
+  long long ref_stride;
+};
+
 }  // namespace avz
 
 extern "C" {
+int avz_launch_scene(const avz::SceneArgs* a, void* stream);
 int avz_launch_chunk_split(const avz::ChunkSplitArgs* a, void* stream);
 int avz_launch_metrics(const avz::MetricsArgs* a, void* stream);
 int avz_launch_chunk_merge(const avz::ChunkMergeArgs* a, void* stream);
