@@ -50,7 +50,7 @@ WORKLOAD_TEXT = {
            "@16 kHz, 4.0 s utterances",
     "ipd": "configs[3]: B={B} utterances/GPU, heuristic IPD mask (masked_mvdr.py), {k} "
            "interferers, 1024-pt STFT hop 512 @16 kHz, 4.0 s utterances",
-    "unet": "configs[4]: B={B} utterances/GPU -> 2-s chunks, U-Net mask (PyTorch-ROCm fp32, "
+    "unet": "configs[4]: B={B} utterances/GPU -> 2-s chunks, U-Net mask (PyTorch-ROCm {unet_dtype}, "
             "random init) -> external-mask MVDR, 1024-pt STFT hop 512, chunk OLA",
 }
 
@@ -67,6 +67,8 @@ def parse():
                     help="time box of the CPU baseline workers")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, available cores)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--unet-dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="unet workload: U-Net forward precision (fp32 = the reference's)")
     ap.add_argument("--rehearse-shared-gpu", action="store_true",
                     help="N > 1 rehearsal on one GPU: all ranks on cuda:0, gloo collectives")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -166,7 +168,8 @@ def setup_unet(args, B, S, dev, mix):
     torch.manual_seed(20250101)
     model = N.FreqPreservingUNet().eval().to(dev)
     n_items = B * -(-S // 16000)
-    bf = N.NeuralMaskBeamformer(model, max_items=n_items)
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[args.unet_dtype]
+    bf = N.NeuralMaskBeamformer(model, max_items=n_items, model_dtype=dt)
     d_mix = torch.from_numpy(mix).to(dev)
     y = {}
 
@@ -338,7 +341,7 @@ def main():
                 "traffic": traffic.get("chain"), "kernel": "avz_mvdr_batch chain",
                 "kernel_ms": step_ms, "alg_bytes_per_launch": alg_chain}
     if rank == 0:
-        cfg = {"workload": WORKLOAD_TEXT[args.workload].format(B=B, k=args.interferers),
+        cfg = {"workload": WORKLOAD_TEXT[args.workload].format(B=B, k=args.interferers, unet_dtype=args.unet_dtype),
                "batch_per_gpu": B, "global_batch": B * world, "samples": S,
                "n_fft": N_FFT, "hop": HOP, "parallelism":
                f"utterance-sharded x{world}, RCCL metric all-reduce only"}
@@ -351,7 +354,7 @@ def main():
         else:
             cfg.update(chunk_items=info["n_items"], tf_bins_per_chunk=info["bins"] // info["n_items"],
                        sigma=1e-5, mask="external (U-Net)", postfilter="max(M, 0.05)",
-                       normalize="none")
+                       normalize="none", unet_dtype=args.unet_dtype)
         line = {
             "metric": METRIC, "value": value, "unit": "TF-bins/s", "n_gpus": world,
             "steps": K, "warmup": args.warmup, "ms_per_step": 1e3 * t_max / K,

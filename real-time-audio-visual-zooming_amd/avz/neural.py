@@ -98,11 +98,16 @@ class NeuralMaskBeamformer:
     ``model``: a [n, 2, F, T] -> [n, F, T] mask network on the device (default:
     FreqPreservingUNet in eval mode). ``model_batch`` bounds the chunks per forward.
     ``model_dtype``: torch.float32 (reference precision) or torch.bfloat16 (the forward
-    runs in bf16, the mask is handed to the HIP chain in fp32)."""
+    runs in bf16, the mask is handed to the HIP chain in fp32). ``channels_last``: NHWC
+    activations for the convolutions (fp32 results equal to within 1e-7 of NCHW on MI355X,
+    ~3 % faster forward; tools/unet_speed.py)."""
 
     def __init__(self, model: nn.Module, max_items: int, conf: dict | None = None,
-                 model_batch: int = 256, model_dtype=torch.float32):
+                 model_batch: int = 256, model_dtype=torch.float32, channels_last: bool = True):
         conf = conf or CONF
+        self.channels_last = channels_last
+        if channels_last:
+            model = model.to(memory_format=torch.channels_last)
         self.model = model
         self.chunk = int(conf["train_seg_samples"])
         self.hop_c = self.chunk // 2
@@ -124,6 +129,8 @@ class NeuralMaskBeamformer:
                           device=items.device)
         for s in range(0, feats.shape[0], self.model_batch):
             x = feats[s:s + self.model_batch]
+            if self.channels_last:
+                x = x.contiguous(memory_format=torch.channels_last)
             if self.model_dtype != torch.float32:
                 with torch.autocast("cuda", dtype=self.model_dtype):
                     out[s:s + len(x)] = self.model(x).float()

@@ -117,6 +117,55 @@ __global__ void __launch_bounds__(NT, 2) bench_x2m(const float* in, float* out, 
   out[blockIdx.x * NT + threadIdx.x] = acc;
 }
 
+
+// Transpose with ds_write_addtid_b32 (address = M0 + offset + 4 * lane, no address VGPR)
+// into planar re/im rows [k][64 + 2 pad] and ds_read_b64 row pairs back.
+template <int OFF>
+__device__ __forceinline__ void addtid_store(float v, unsigned m0) {
+  asm volatile("s_mov_b32 m0, %1\n\tds_write_addtid_b32 %0 offset:%2"
+               :: "v"(v), "s"(m0), "i"(OFF) : "memory", "m0");
+}
+__device__ __forceinline__ void transpose_addtid(cf (&v)[32], unsigned base, const float* plane,
+                                                 int l, int g) {
+  static_for<0, 32>([&](auto k) {
+    addtid_store<k * 264>(v[k].x, base);
+    addtid_store<8448 + k * 264>(v[k].y, base);
+  });
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const float* re = plane + l * 66 + 32 * g;
+  const float* im = re + 2112;
+  static_for<0, 16>([&](auto q) {
+    const float2 a = *reinterpret_cast<const float2*>(re + 2 * q);
+    const float2 b = *reinterpret_cast<const float2*>(im + 2 * q);
+    v[2 * q] = {a.x, b.x};
+    v[2 * q + 1] = {a.y, b.y};
+  });
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT, 2) bench_x2_addtid(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 5, l = lane & 31;
+  cf* tw = reinterpret_cast<cf*>(lds + (NT / 64) * 16896);
+  Fft1024x2::fill_twiddles(tw, threadIdx.x, NT);
+  Fft1024x2 f; f.init(lane);
+  unsigned char* wbase = lds + wave * 16896;
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)wbase);
+  cf v[32];
+  static_for<0, 32>([&](auto r) { v[r] = {in[(l + 32 * r) & 1023], in[(l + 32 * r + 7) & 1023]}; });
+  __syncthreads();
+  float acc = 0;
+  for (int it = 0; it < iters; ++it) {
+    f.stage1(v, tw);
+    transpose_addtid(v, m0, reinterpret_cast<const float*>(wbase), l, g);
+    f.stage2(v);
+  }
+  static_for<0, 32>([&](auto k) { acc += v[k].x + v[k].y; });
+  out[blockIdx.x * NT + threadIdx.x] = acc;
+}
+
 extern "C" int run_bench(int variant, const float* in, float* out, int blocks, int iters) {
   switch (variant) {
     case 0: { auto k = bench_x2<512>; int lds = 8 * 16896 + 8192;
@@ -129,6 +178,9 @@ extern "C" int run_bench(int variant, const float* in, float* out, int blocks, i
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, 0, in, out, iters); break; }
     case 3: { auto k = bench_x2<256>; int lds = 4 * 16896 + 8192;
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
+    case 9: { auto k = bench_x2_addtid<256>; int lds = 4 * 16896 + 8192;
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
     case 4: case 5: case 6: case 7: case 8: { auto k = variant == 4 ? bench_x2m<256, 0> : variant == 5 ? bench_x2m<256, 1> : variant == 6 ? bench_x2m<256, 2> : variant == 7 ? bench_x2m<256, 3> : bench_x2m<256, 4>;
