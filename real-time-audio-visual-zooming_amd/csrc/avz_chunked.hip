@@ -235,7 +235,9 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
       else
         window_fft_reg(v, wc, fft, my_spec, tw_reg, lm);
     }
+    AVZ_STAMP(3);
     if (step + 1 < nstep) issue_loads(step + 1);
+    AVZ_STAMP(11);
     lds_barrier();
     AVZ_STAMP(1);
     const int nvalid = min(FB, T - f0);
@@ -300,6 +302,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
       const unsigned long long bal = __ballot(noise);
       nyq_bits |= ((uint32_t)bal & ((1u << FB) - 1u)) << (step * FB);
     }
+    AVZ_STAMP(12);
     lds_barrier();
     AVZ_STAMP(2);
   }

@@ -34,7 +34,7 @@ static __device__ unsigned long long* g_stamps;
   do {                                                                      \
     if (threadIdx.x == 0 && g_stamps) {                                     \
       const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();     \
-      g_stamps[(blockIdx.y * gridDim.x + blockIdx.x) * 16 + (i)] += now_ - stamp_prev;                 \
+      atomicAdd(g_stamps + (blockIdx.y * gridDim.x + blockIdx.x) * 16 + (i), now_ - stamp_prev); \
       stamp_prev = now_;                                                    \
     }                                                                       \
   } while (0)

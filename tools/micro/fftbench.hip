@@ -2,14 +2,8 @@
 // LDS transpose -> natural-order spectrum store -> block barrier} ITERS times.
 // Reports nothing itself; time it from Python (tools/micro/fftbench.py).
 #include <hip/hip_runtime.h>
-#include "../../real-time-audio-visual-zooming_amd/csrc/avz_fft.hpp"
+#include "../../real-time-audio-visual-zooming_amd/csrc/avz_common.hpp"
 using namespace avz;
-
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 
 template <int NT>
 __global__ void __launch_bounds__(NT, 1) bench_x2(const float* in, float* out, int iters) {
@@ -166,6 +160,141 @@ __global__ void __launch_bounds__(NT, 2) bench_x2_addtid(const float* in, float*
   out[blockIdx.x * NT + threadIdx.x] = acc;
 }
 
+// ---------------------------------------------------------------------------
+// Variant 10: "pair-output" second stage. After the transpose, lane l of a group reads
+// row l (k1 = l) for the even outputs and row l' = (32 - l) % 32 for the odd ones
+// (first DIF radix-2 stage folded into the reads), so its registers end up holding
+// complete (k, N - k) bin pairs: no spectrum round trip through LDS, no block barrier.
+// Group 0 transforms the mic pair, group 1 the reference pair of the same frame; one
+// permlane32 swap per register gives every lane mic + reference for 8 bins, which it
+// splits, masks (IBM) and accumulates like the analysis bin phase.
+__device__ __forceinline__ void swap32(cf& a, cf& b) {
+  auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+  auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+  a = {__uint_as_float(rx[0]), __uint_as_float(ry[0])};
+  b = {__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+}
+
+template <int NT, bool TWREG>
+__global__ void __launch_bounds__(NT, 2) bench_pairs(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 5, l = lane & 31;
+  cf* tw = reinterpret_cast<cf*>(lds + (NT / 64) * 16896);
+  Fft1024x2::fill_twiddles(tw, threadIdx.x, NT);
+  Fft1024x2 f; f.init(lane);
+  cf* scr = reinterpret_cast<cf*>(lds + wave * 16896 + g * 8448);
+  cf v[32];
+  static_for<0, 32>([&](auto r) { v[r] = {in[(l + 32 * r + g) & 1023], in[(l + 32 * r + 7) & 1023]}; });
+  __syncthreads();
+  cf twr[31];
+  if constexpr (TWREG) f.load_twiddles(twr, tw);
+  const int lp = (32 - l) & 31;
+  const bool l0 = (l == 0);
+  Acc32 acc[8];
+  uint32_t bits[8];
+  static_for<0, 8>([&](auto s) { acc[s].zero(); bits[s] = 0u; });
+  for (int it = 0; it < iters; ++it) {
+    if constexpr (TWREG) f.stage1_reg(v, twr); else f.stage1(v, tw);
+    static_for<0, 32>([&](auto k) { scr[k * 33 + l] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    cf e[16], o[16];
+    static_for<0, 16>([&](auto n) {
+      const cf a = scr[l * 33 + n], b = scr[l * 33 + n + 16];
+      const cf c = scr[lp * 33 + n], d = scr[lp * 33 + n + 16];
+      e[n] = c_add(a, b);
+      o[n] = w32mul<n>(c_sub(c, d));
+    });
+    __builtin_amdgcn_wave_barrier();
+    dft16(e);
+    dft16(o);
+    cf zk[16], zn[16];
+    static_for<0, 16>([&](auto s) {
+      if constexpr (s < 8) {
+        zk[s] = e[s];
+        const cf a = e[(16 - s) % 16], b = o[15 - s];
+        zn[s] = {l0 ? a.x : b.x, l0 ? a.y : b.y};
+      } else {
+        const cf a = o[s - 8], b = e[s];
+        zk[s] = {l0 ? a.x : b.x, l0 ? a.y : b.y};
+        const cf c = o[23 - s], d = o[15 - s];
+        zn[s] = {l0 ? c.x : d.x, l0 ? c.y : d.y};
+      }
+    });
+    static_for<0, 8>([&](auto s) { swap32(zk[s], zk[s + 8]); swap32(zn[s], zn[s + 8]); });
+    // slot s: mic pair (zk[s], zn[s]), reference pair (zk[s+8], zn[s+8])
+    static_for<0, 8>([&](auto s) {
+      cf x0, x1;
+      split_pair2(zk[s], zn[s], x0, x1);
+      const cf zr = zk[s + 8], zrp = zn[s + 8];
+      const float tr = zr.x + zrp.x, ti = zr.y - zrp.y;
+      const float ir = zr.y + zrp.y, ii = zr.x - zrp.x;
+      const bool noise = ir * ir + ii * ii > tr * tr + ti * ti;
+      const float wgt = noise ? 1.0f : 0.0f;
+      bits[s] |= (noise ? 1u : 0u) << (it & 31);
+      acc[s].add(x0, x1, wgt, wgt);
+    });
+    // next input: the spectra (keeps the data dependent)
+    static_for<0, 16>([&](auto r) { v[r] = e[r]; v[r + 16] = o[r]; });
+  }
+  float a = 0;
+  static_for<0, 8>([&](auto s) { a += acc[s].c00 + acc[s].c11 + acc[s].c01r + acc[s].c01i + acc[s].cm + (float)bits[s]; });
+  static_for<0, 32>([&](auto k) { a += v[k].x + v[k].y; });
+  out[blockIdx.x * NT + threadIdx.x] = a;
+}
+
+// Variant 11: the current analysis pattern with its bin phase: 8 FFTs per block step
+// (waves 0-1 mic frames, 2-3 reference frames), natural-order spectra to LDS, block
+// barrier, thread-per-bin (2 bins x 4 frames) split / IBM mask / covariance, barrier.
+template <int NT, bool TWREG>
+__global__ void __launch_bounds__(NT, 2) bench_binphase(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 5, l = lane & 31;
+  cf* tw = reinterpret_cast<cf*>(lds + (NT / 64) * 16896);
+  Fft1024x2::fill_twiddles(tw, threadIdx.x, NT);
+  Fft1024x2 f; f.init(lane);
+  cf* scr = reinterpret_cast<cf*>(lds + wave * 16896 + g * 8448);
+  cf v[32];
+  static_for<0, 32>([&](auto r) { v[r] = {in[(l + 32 * r + g) & 1023], in[(l + 32 * r + 7) & 1023]}; });
+  __syncthreads();
+  cf twr[31];
+  if constexpr (TWREG) f.load_twiddles(twr, tw);
+  Acc32 acc[2];
+  uint32_t bits[2] = {0u, 0u};
+  acc[0].zero(); acc[1].zero();
+  auto slot = [&](int s) { return reinterpret_cast<const cf*>(lds + (s >> 1) * 16896 + (s & 1) * 8448); };
+  for (int it = 0; it < iters; ++it) {
+    if constexpr (TWREG) f.forward_reg(v, scr, twr); else f.forward(v, scr, tw);
+    static_for<0, 32>([&](auto k) { scr[l + 32 * k] = v[k]; });
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kb = tid + j * NT, kp = (1024 - kb) & 1023;
+      cf zm[4], zmp[4], zr[4], zrp[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        zm[i] = slot(i)[kb]; zmp[i] = slot(i)[kp];
+        zr[i] = slot(4 + i)[kb]; zrp[i] = slot(4 + i)[kp];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        cf x0, x1;
+        split_pair2(zm[i], zmp[i], x0, x1);
+        const float tr = zr[i].x + zrp[i].x, ti = zr[i].y - zrp[i].y;
+        const float ir = zr[i].y + zrp[i].y, ii = zr[i].x - zrp[i].x;
+        const bool noise = ir * ir + ii * ii > tr * tr + ti * ti;
+        const float wgt = noise ? 1.0f : 0.0f;
+        bits[j] |= (noise ? 1u : 0u) << ((4 * it + i) & 31);
+        acc[j].add(x0, x1, wgt, wgt);
+      }
+    }
+    lds_barrier();
+  }
+  float a = 0;
+  static_for<0, 2>([&](auto s) { a += acc[s].c00 + acc[s].c11 + acc[s].c01r + acc[s].c01i + acc[s].cm + (float)bits[s]; });
+  static_for<0, 32>([&](auto k) { a += v[k].x + v[k].y; });
+  out[blockIdx.x * NT + threadIdx.x] = a;
+}
+
 extern "C" int run_bench(int variant, const float* in, float* out, int blocks, int iters) {
   switch (variant) {
     case 0: { auto k = bench_x2<512>; int lds = 8 * 16896 + 8192;
@@ -181,6 +310,12 @@ extern "C" int run_bench(int variant, const float* in, float* out, int blocks, i
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
     case 9: { auto k = bench_x2_addtid<256>; int lds = 4 * 16896 + 8192;
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
+    case 10: case 11: case 12: case 13: {
+      auto k = variant == 10 ? bench_pairs<256, false> : variant == 11 ? bench_binphase<256, false>
+             : variant == 12 ? bench_pairs<256, true> : bench_binphase<256, true>;
+      int lds = 4 * 16896 + 8192;
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
     case 4: case 5: case 6: case 7: case 8: { auto k = variant == 4 ? bench_x2m<256, 0> : variant == 5 ? bench_x2m<256, 1> : variant == 6 ? bench_x2m<256, 2> : variant == 7 ? bench_x2m<256, 3> : bench_x2m<256, 4>;

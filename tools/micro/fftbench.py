@@ -15,9 +15,11 @@ names = {0: "x2 (32 pts/lane), 8 waves/block", 1: "x1 (16 pts/lane), 16 waves/bl
          2: "x1 (16 pts/lane), 8 waves/block", 3: "x2, 4 waves/block (x2 blocks/CU)",
          4: "x2 FFT only, 4 waves/block", 5: "x2 + bpermute/swap bins, 4 w/b",
          6: "x2 + wave-local LDS spectrum, 4 w/b", 7: "x2 arithmetic + LDS twiddles, no transpose",
-         8: "x2 arithmetic only (no LDS at all)", 9: "x2 FFT only, addtid planar transpose"}
-ffts_per_block = {0: 16, 1: 16, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 8, 9: 8}
-for v, blocks in ((4, 512), (9, 512), (4, 512), (9, 512), (7, 512), (8, 512)):
+         8: "x2 arithmetic only (no LDS at all)", 9: "x2 FFT only, addtid planar transpose",
+         10: "pairs: FFT + in-register IBM bins, LDS tw", 11: "current: FFT + LDS bin phase, LDS tw",
+         12: "pairs, register twiddles", 13: "current, register twiddles"}
+ffts_per_block = {0: 16, 1: 16, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 8, 9: 8, 10: 8, 11: 8, 12: 8, 13: 8}
+for v, blocks in ((11, 512), (10, 512), (13, 512), (12, 512), (11, 512), (10, 512), (4, 512)):
     for _ in range(2):
         lib.run_bench(v, inp.data_ptr(), out.data_ptr(), blocks, iters)
     torch.cuda.synchronize()

@@ -26,8 +26,9 @@ if FUSED:  # avz_kernels.hip, one block per utterance
     PHASES = ["p1 FFT rest", "p1 bins", "solve", "p2 FFT rest", "p2 bins", "iFFT", "OLA",
               "peak/norm", "load wait", "fft stage1", "fft transp", "fft stage2"]
 else:  # avz_chunked.hip: analysis 0-3, synthesis 4-10, one block per (chunk, utterance)
-    PHASES = ["A load wait", "A FFT", "A bins", "A partials", "S prologue", "S load wait",
-              "S FFT", "S apply", "S iFFT", "S OLA", "S peak"]
+    PHASES = ["A load wait", "A barrier 1", "A barrier 2", "A window+FFT", "S prologue",
+              "S load wait", "S FFT", "S apply", "S iFFT", "S OLA", "S peak", "A load issue",
+              "A bins"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=256)
