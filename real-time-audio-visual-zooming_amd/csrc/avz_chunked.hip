@@ -243,9 +243,12 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     const int nvalid = min(FB, T - f0);
     // Thread-per-bin over the step's frames. A full step runs unguarded so all of its
     // LDS reads can issue back to back; only a chunk's last step may be partial.
+    uint32_t ipd_fix[BPT];
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) ipd_fix[j] = 0u;
     auto bin_phase = [&](auto full) {
       // frames whose reads are batched together (IPD: one, its inlined atan2f fallback is big)
-      constexpr int G = (MASK == MASK_IPD) ? 1 : (FB < 4 ? FB : 4);
+      constexpr int G = FB < 4 ? FB : 4;
 #pragma unroll
       for (int j = 0; j < BPT; ++j) {
         const int kb = tid + j * NT;
@@ -271,6 +274,14 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
             if (decltype(full)::value || g0 + i < nvalid) {
               cf x0, x1;
               split_pair2(zm[i], zmp[i], x0, x1);  // 2 y0, 2 y1
+              if constexpr (MASK == MASK_IPD) {
+                // the exact angle test of near-colinear bins runs after the loop
+                const bool clear = ipd_clear(x0, x1);
+                const float w = clear ? 1.0f : 0.0f;
+                ipd_fix[j] |= (clear ? 0u : 1u) << (g0 + i);
+                acc[j].add(x0, x1, w, w);
+                continue;
+              }
               bool noise = false;
               float wgt;
               const float m =
@@ -287,6 +298,25 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
       bin_phase(std::true_type{});
     else
       bin_phase(std::false_type{});
+    if constexpr (MASK == MASK_IPD) {
+      // Near-colinear (bin, frame) pairs (always DC, rarely any other): exact weight from
+      // the spectra still in LDS. Waves with no such lane skip this.
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) {
+        const int kb = tid + j * NT;
+        const int kp = (N - kb) & (N - 1);
+        uint32_t f = ipd_fix[j];
+        while (f) {
+          const int i = __builtin_ctz(f);
+          f &= f - 1u;
+          const cf* Zm = slot_ptr<N>(lds, i);
+          cf x0, x1;
+          split_pair2(Zm[kb], Zm[kp], x0, x1);
+          const float w = ipd_weight_exact(x0, x1);
+          acc[j].add(x0, x1, w, w);
+        }
+      }
+    }
     if (nyq_wave) {
       bool noise = false;
       if (lane < nvalid) {

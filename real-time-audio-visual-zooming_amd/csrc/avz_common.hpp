@@ -148,13 +148,24 @@ __device__ __forceinline__ void split_self(cf z, cf& a, cf& b) {
 
 // Heuristic phase mask (masked_mvdr.py:37-46): 0.01 where angle(Y0) == angle(Y1)
 // as float32, else 1.0. A cross-product test settles every bin whose angles differ
-// by far more than an fp32 ulp; the rest compare atan2f exactly.
-__device__ __forceinline__ float ipd_weight(cf a, cf b) {
+// by far more than an fp32 ulp. Real bins (DC / Nyquist: imaginary parts exactly +0
+// from split_pair2) have angle +0 or +pi by the sign bit of the real part, exactly as
+// atan2f(+0, x); only the rare near-colinear complex bins reach atan2f, so a wave
+// skips that code unless one of its lanes needs it.
+__device__ __forceinline__ bool ipd_clear(cf a, cf b) {  // angles certainly differ
   const float cr = a.y * b.x - a.x * b.y;
   const float n2 = (a.x * a.x + a.y * a.y) * (b.x * b.x + b.y * b.y);
-  if (cr * cr > 1e-10f * n2) return 1.0f;
+  return cr * cr > 1e-10f * n2;
+}
+__device__ __forceinline__ float ipd_weight_exact(cf a, cf b) {
+  const unsigned ia = __float_as_uint(a.y), ib = __float_as_uint(b.y);
+  if ((ia | ib) == 0u)  // both imaginary parts +0
+    return (signbit(a.x) == signbit(b.x)) ? 0.01f : 1.0f;
   const float pa = atan2f(a.y, a.x), pb = atan2f(b.y, b.x);
   return (fabsf(pa - pb) > 0.0f) ? 1.0f : 0.01f;
+}
+__device__ __forceinline__ float ipd_weight(cf a, cf b) {
+  return ipd_clear(a, b) ? 1.0f : ipd_weight_exact(a, b);
 }
 
 struct Acc32 {
