@@ -157,7 +157,7 @@ def setup_chain(args, B, S, dev, mix, tgt, itf):
     info = dict(plan=plan, out=out[:, :min(n_out, S)], bins=B * F * T,
                 alg_analysis=B * streams * S * 4, alg_chain=B * (streams * S * 4 + n_out * 4),
                 kernel=f"avz_analysis_kernel<1024,{'IBM' if args.workload == 'ibm' else 'IPD'}>",
-                mix=d_mix)
+                mix=d_mix, refs=refs, host=(mix, tgt, itf))
     return step, info
 
 
@@ -268,6 +268,35 @@ def main():
         extra["unet_ms"] = e0.elapsed_time(e1) / max(1, K // 2)
         extra["mvdr_chain_ms"] = chain_ms
         extra["mvdr_chain_tf_bins_per_s"] = info["bins"] / (chain_ms * 1e-3)
+
+    if args.workload != "unet" and rank == 0:
+        try:
+            # PCIe-inclusive rate (not `value`): the same step with its inputs copied from
+            # pinned host memory first and the output copied back (host-buffer callers, e.g.
+            # the oracle_debug.main mirror). Reported beside the HBM-resident number.
+            pin = lambda x: torch.from_numpy(x).pin_memory()  # noqa: E731
+            ho = torch.empty(tuple(info["out"].shape), dtype=torch.float32).pin_memory()
+            d_in = [(pin(info["host"][0]), info["mix"])]
+            if info["refs"]:
+                d_in += [(pin(info["host"][1]), info["refs"]["ref_tgt"]),
+                         (pin(info["host"][2]), info["refs"]["ref_int"])]
+            n_pcie = max(2, K // 4)
+            torch.cuda.synchronize()
+            p0 = time.perf_counter()
+            for _ in range(n_pcie):
+                for h, d in d_in:
+                    d.copy_(h, non_blocking=True)
+                step()
+                ho.copy_(info["out"], non_blocking=True)
+            torch.cuda.synchronize()
+            pcie_ms = 1e3 * (time.perf_counter() - p0) / n_pcie
+            h2d = sum(h.numel() * 4 for h, _ in d_in)
+            extra["pcie_inclusive"] = {"ms_per_step": pcie_ms,
+                                       "tf_bins_per_s": info["bins"] / (pcie_ms * 1e-3),
+                                       "h2d_bytes": h2d, "d2h_bytes": ho.numel() * 4,
+                                       "note": "rank 0; not the headline value"}
+        except Exception as exc:  # a side figure must never sink the bench line
+            extra["pcie_inclusive"] = {"error": repr(exc)[:200]}
 
     # ---- final metrics: projection SIR per utterance (run_metrics.py:6-36), RCCL all-reduce
     L = S
