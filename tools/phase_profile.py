@@ -21,14 +21,10 @@ import torch  # noqa: E402
 import avz  # noqa: E402
 from avz import synth  # noqa: E402
 
-FUSED = os.environ.get("AVZ_KERNEL_PATH") == "fused"
-if FUSED:  # avz_kernels.hip, one block per utterance
-    PHASES = ["p1 FFT rest", "p1 bins", "solve", "p2 FFT rest", "p2 bins", "iFFT", "OLA",
-              "peak/norm", "load wait", "fft stage1", "fft transp", "fft stage2"]
-else:  # avz_chunked.hip: analysis 0-3, synthesis 4-10, one block per (chunk, utterance)
-    PHASES = ["A load wait", "A barrier 1", "A barrier 2", "A window+FFT", "S prologue",
-              "S load wait", "S FFT", "S apply", "S iFFT", "S OLA", "S peak", "A load issue",
-              "A bins"]
+# avz_chunked.hip stamp slots: analysis 0-3, 11, 12; synthesis 4-10
+PHASES = ["A load wait", "A barrier 1", "A barrier 2", "A window+FFT", "S prologue",
+          "S load wait", "S FFT", "S apply", "S iFFT", "S OLA", "S peak", "A load issue",
+          "A bins"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=256)
@@ -45,10 +41,10 @@ plan = avz.MVDRPlan(n_fft=a.n_fft, sigma=1.0, mic_d=0.01, mask=a.mask,
                     max_batch=a.batch, max_samples=S)
 d = [torch.from_numpy(x).to(dev) for x in (mix, tgt, itf)]
 kw = dict(ref_tgt=d[1], ref_int=d[2]) if a.mask == "ibm" else {}
-nblk = a.batch if FUSED else a.batch * -(-plan.frames(S) // avz._lib.lib.avz_chunk_frames())
+nblk = a.batch * -(-plan.frames(S) // avz._lib.lib.avz_chunk_frames())
 st = torch.zeros((nblk, 16), dtype=torch.int64, device=dev)
 lib = avz._lib.lib
-setter = lib.avz_debug_set_stamps if FUSED else lib.avz_debug_set_stamps_chunked
+setter = lib.avz_debug_set_stamps_chunked
 setter.argtypes = [ct.c_void_p]
 for _ in range(3):
     plan.run(d[0], **kw)
