@@ -60,6 +60,7 @@ e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / reps
 us = st.double().cpu().numpy() / reps / 100.0  # 100 MHz ticks -> us
+us = us[us.sum(axis=1) > 0]  # persistent grids: only the launched blocks' rows
 tot = us.sum(axis=1)
 print(f"kernel {ms*1e3:.1f} us/launch (stamped build), B={a.batch}, N={a.n_fft}, mask={a.mask}")
 print(f"per-block stamped total: mean {tot.mean():.1f} us, min {tot.min():.1f}, max {tot.max():.1f}")
