@@ -46,12 +46,12 @@ N_FFT, HOP, FS, SECONDS = 1024, 512, 16000, 4.0
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 DEFAULT_BATCH = {"ibm": 256, "ipd": 1024, "unet": 1024}
 WORKLOAD_TEXT = {
-    "ibm": "configs[1]: B={B} utterances/GPU, {k} interferers, oracle IBM, 1024-pt STFT hop 512 "
+    "ibm": "configs[1]: B={B} utterances/GPU, {k} interferers, oracle IBM, {n}-pt STFT hop {h} "
            "@16 kHz, 4.0 s utterances",
     "ipd": "configs[3]: B={B} utterances/GPU, heuristic IPD mask (masked_mvdr.py), {k} "
-           "interferers, 1024-pt STFT hop 512 @16 kHz, 4.0 s utterances",
+           "interferers, {n}-pt STFT hop {h} @16 kHz, 4.0 s utterances",
     "unet": "configs[4]: B={B} utterances/GPU -> 2-s chunks, U-Net mask (PyTorch-ROCm {unet_dtype}, "
-            "random init) -> external-mask MVDR, 1024-pt STFT hop 512, chunk OLA",
+            "random init) -> external-mask MVDR, {n}-pt STFT hop {h}, chunk OLA",
 }
 
 
@@ -67,6 +67,8 @@ def parse():
                     help="time box of the CPU baseline workers")
     ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, available cores)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--n-fft", type=int, choices=(512, 1024), default=1024,
+                    help="STFT size (hop n/2); 1024 is the BASELINE configs, 512 oracle_debug's default")
     ap.add_argument("--unet-dtype", choices=("fp32", "bf16"), default="fp32",
                     help="unet workload: U-Net forward precision (fp32 = the reference's)")
     ap.add_argument("--rehearse-shared-gpu", action="store_true",
@@ -124,7 +126,7 @@ def cpu_baseline(sample, seconds, workers, workload):
             "kind": "port",
             "sample": (f"time-boxed {seconds:.0f} s x {workers} single-threaded workers over "
                        f"{sample[0].shape[0]} distinct utterances of the same workload (4.0 s, "
-                       f"1024/512): {utts} utterances; {what} minus WAV I/O; wall {wall:.1f} s")}
+                       f"{N_FFT}/{HOP}): {utts} utterances; {what} minus WAV I/O; wall {wall:.1f} s")}
 
 
 # ----------------------------------------------------------------------------- workloads
@@ -156,7 +158,7 @@ def setup_chain(args, B, S, dev, mix, tgt, itf):
     F, T = N_FFT // 2 + 1, -(-S // HOP) + 1
     info = dict(plan=plan, out=out[:, :min(n_out, S)], bins=B * F * T,
                 alg_analysis=B * streams * S * 4, alg_chain=B * (streams * S * 4 + n_out * 4),
-                kernel=f"avz_analysis_kernel<1024,{'IBM' if args.workload == 'ibm' else 'IPD'}>",
+                kernel=f"avz_analysis_kernel<{N_FFT},{'IBM' if args.workload == 'ibm' else 'IPD'}>",
                 mix=d_mix, refs=refs, host=(mix, tgt, itf))
     return step, info
 
@@ -182,12 +184,14 @@ def setup_unet(args, B, S, dev, mix):
     info = dict(plan=bf.plan, bf=bf, bins=n_items * F * Tc, n_items=n_items,
                 alg_analysis=n_items * 2 * bf.chunk * 4,
                 alg_chain=n_items * (2 * bf.chunk * 4 + n_out * 4),
-                kernel="avz_analysis_kernel<1024,EXTERNAL>", mix=d_mix, y=y)
+                kernel=f"avz_analysis_kernel<{N_FFT},EXTERNAL>", mix=d_mix, y=y)
     return step, info
 
 
 def main():
+    global N_FFT, HOP
     args = parse()
+    N_FFT, HOP = args.n_fft, args.n_fft // 2
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -370,7 +374,8 @@ def main():
                 "traffic": traffic.get("chain"), "kernel": "avz_mvdr_batch chain",
                 "kernel_ms": step_ms, "alg_bytes_per_launch": alg_chain}
     if rank == 0:
-        cfg = {"workload": WORKLOAD_TEXT[args.workload].format(B=B, k=args.interferers, unet_dtype=args.unet_dtype),
+        cfg = {"workload": WORKLOAD_TEXT[args.workload].format(
+            B=B, k=args.interferers, unet_dtype=args.unet_dtype, n=N_FFT, h=HOP),
                "batch_per_gpu": B, "global_batch": B * world, "samples": S,
                "n_fft": N_FFT, "hop": HOP, "parallelism":
                f"utterance-sharded x{world}, RCCL metric all-reduce only"}
