@@ -206,3 +206,32 @@ def test_plan_rejects_bad_shapes(avz, gpu_device):
         plan.run(x[:, :, :2048])                             # IBM without references
     with pytest.raises(avz.AvzError):
         avz.MVDRPlan(n_fft=768)
+
+
+# ----------------------------------------------------------------------------- IPD ties
+def test_ipd_identical_channels(avz, gpu_device):
+    """Degenerate IPD input: both channels identical, so masked_mvdr.py:37-46 sees
+    bitwise-equal angles in every bin and weights them all 0.01. The HIP path transforms
+    the two channels as one packed complex FFT, whose split does not reproduce
+    bitwise-equal channel spectra: every (bin, frame) reaches the exact-angle fix-up
+    pass and most come out 1.0 (documented deviation; measured: mask sums
+    ~100x the reference's). The output is unaffected — with identical channels R is
+    rank one and the MVDR weights at broadside do not depend on the mask weighting —
+    and is checked against the oracle at the usual tolerance."""
+    mix, tgt, itf = triple_f32("test")
+    n = 1024
+    mono = np.ascontiguousarray(np.stack([mix[0], mix[0]]))
+    plan = avz.MVDRPlan(n_fft=n, sigma=1e-7, mic_d=0.01, mask="ipd", postfilter="none",
+                        normalize="peak", norm_eps=1e-6, max_batch=1, max_samples=mono.shape[1])
+    F = n // 2 + 1
+    cov = torch.zeros((1, F, 5), dtype=torch.float64, device=gpu_device)
+    out, _ = plan.run(dev_t(mono, gpu_device)[None], cov_out=cov)
+    torch.cuda.synchronize()
+    out = out[0, :plan.out_len(mono.shape[1])].cpu().numpy().astype(np.float64)
+    ref, st = O.masked_mvdr_vec(mono, n_fft=n, hop=n // 2, return_stages=True)
+    # sum of mask weights per bin (cov column 4) vs the reference's
+    msum = cov[0, :, 4].cpu().numpy()
+    rsum = st["mask"].sum(axis=1)
+    print(f"identical channels: max |mask sum - ref| = {np.max(np.abs(msum - rsum)):.3g} "
+          f"(ref sum per bin {rsum[10]:.3g}), max |out - ref| = {np.max(np.abs(out - ref)):.3g}")
+    assert np.max(np.abs(out - ref)) <= WAVE_TOL
