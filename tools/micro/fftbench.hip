@@ -295,6 +295,154 @@ __global__ void __launch_bounds__(NT, 2) bench_binphase(const float* in, float* 
   out[blockIdx.x * NT + threadIdx.x] = a;
 }
 
+// Variants 14-16: the analysis step pattern (variant 13: register twiddles, spectrum
+// round trip, thread-per-bin IBM bin phase) plus the next step's sample loads, 2 x 32
+// dwords per lane issued after the FFT like avz_analysis_kernel. MODE 1: streaming from a
+// 512 KB region per block (HBM / MALL); MODE 2: from a 16 KB region per block (cache
+// resident); MODE 3: as 1 but the loaded values only feed a side sum, not the next FFT.
+template <int NT, int MODE>
+__global__ void __launch_bounds__(NT, 2) bench_binphase_loads(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 5, l = lane & 31;
+  cf* tw = reinterpret_cast<cf*>(lds + (NT / 64) * 16896);
+  Fft1024x2::fill_twiddles(tw, threadIdx.x, NT);
+  Fft1024x2 f; f.init(lane);
+  cf* scr = reinterpret_cast<cf*>(lds + wave * 16896 + g * 8448);
+  constexpr int REGION = (MODE == 2) ? 4096 : 131072;  // floats per block
+  const float* src = in + (size_t)blockIdx.x * REGION;
+  cf v[32];
+  static_for<0, 32>([&](auto r) { v[r] = {src[l + 32 * r], src[REGION / 2 + l + 32 * r]}; });
+  __syncthreads();
+  cf twr[31];
+  f.load_twiddles(twr, tw);
+  Acc32 acc[2];
+  uint32_t bits[2] = {0u, 0u};
+  acc[0].zero(); acc[1].zero();
+  float side = 0.f;
+  cf w[32];
+  auto slot = [&](int s) { return reinterpret_cast<const cf*>(lds + (s >> 1) * 16896 + (s & 1) * 8448); };
+  for (int it = 0; it < iters; ++it) {
+    if constexpr (MODE == 3) { static_for<0, 32>([&](auto r) { side += w[r].x + w[r].y; }); }
+    f.forward_reg(v, scr, twr);
+    static_for<0, 32>([&](auto k) { scr[l + 32 * k] = v[k]; });
+    {
+      const int fr = (it + 1) * 8 + wave * 2 + g;
+      const int off = (fr * 512) % (REGION / 2 - 1024);
+      if constexpr (MODE == 3) {
+        static_for<0, 32>([&](auto r) { w[r] = {src[off + l + 32 * r], src[REGION / 2 + off + l + 32 * r]}; });
+      } else if constexpr (MODE == 4) {  // dwordx2: half the instructions, same bytes
+        static_for<0, 32>([&](auto r) {
+          const float2 t = *reinterpret_cast<const float2*>(src + off + 2 * (l + 32 * r));
+          v[r] = {t.x, t.y};
+        });
+      } else if constexpr (MODE == 5) {  // one channel: half the instructions and bytes
+        static_for<0, 32>([&](auto r) { v[r].x = src[off + l + 32 * r]; });
+      } else if constexpr (MODE == 6) {  // an eighth of the loads
+        static_for<0, 4>([&](auto r) { v[r] = {src[off + l + 32 * r], src[REGION / 2 + off + l + 32 * r]}; });
+      } else {
+        static_for<0, 32>([&](auto r) { v[r] = {src[off + l + 32 * r], src[REGION / 2 + off + l + 32 * r]}; });
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kb = tid + j * NT, kp = (1024 - kb) & 1023;
+      cf zm[4], zmp[4], zr[4], zrp[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        zm[i] = slot(i)[kb]; zmp[i] = slot(i)[kp];
+        zr[i] = slot(4 + i)[kb]; zrp[i] = slot(4 + i)[kp];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        cf x0, x1;
+        split_pair2(zm[i], zmp[i], x0, x1);
+        const float tr = zr[i].x + zrp[i].x, ti = zr[i].y - zrp[i].y;
+        const float ir = zr[i].y + zrp[i].y, ii = zr[i].x - zrp[i].x;
+        const bool noise = ir * ir + ii * ii > tr * tr + ti * ti;
+        const float wgt = noise ? 1.0f : 0.0f;
+        bits[j] |= (noise ? 1u : 0u) << ((4 * it + i) & 31);
+        acc[j].add(x0, x1, wgt, wgt);
+      }
+    }
+    lds_barrier();
+  }
+  float a = side;
+  static_for<0, 2>([&](auto s) { a += acc[s].c00 + acc[s].c11 + acc[s].c01r + acc[s].c01i + acc[s].cm + (float)bits[s]; });
+  static_for<0, 32>([&](auto k) { a += v[k].x + v[k].y; });
+  out[blockIdx.x * NT + threadIdx.x] = a;
+}
+
+// Variant 20: as variant 18 (one channel's loads) but double-buffered: the loads of step
+// it + 2 are issued after step it's FFT into the buffer it just consumed.
+template <int NT, bool DB>
+__global__ void __launch_bounds__(NT, 2) bench_binphase_db(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 5, l = lane & 31;
+  cf* tw = reinterpret_cast<cf*>(lds + (NT / 64) * 16896);
+  Fft1024x2::fill_twiddles(tw, threadIdx.x, NT);
+  Fft1024x2 f; f.init(lane);
+  cf* scr = reinterpret_cast<cf*>(lds + wave * 16896 + g * 8448);
+  constexpr int REGION = 131072;
+  const float* src = in + (size_t)blockIdx.x * REGION;
+  float ba[32], bb[32];
+  auto load = [&](float (&b)[32], int it) {
+    const int fr = it * 8 + wave * 2 + g;
+    const int off = (fr * 512) % (REGION / 2 - 1024);
+    static_for<0, 32>([&](auto r) { b[r] = src[off + l + 32 * r]; });
+  };
+  load(ba, 0);
+  if (DB) load(bb, 1);
+  __syncthreads();
+  Acc32 acc[2];
+  uint32_t bits[2] = {0u, 0u};
+  acc[0].zero(); acc[1].zero();
+  auto slot = [&](int s) { return reinterpret_cast<const cf*>(lds + (s >> 1) * 16896 + (s & 1) * 8448); };
+  cf v[32];
+  static_for<0, 32>([&](auto r) { v[r] = {0.f, 0.f}; });
+  auto step = [&](float (&b)[32], int it) {
+    static_for<0, 32>([&](auto r) { v[r].x += b[r]; });
+    f.forward(v, scr, tw);
+    static_for<0, 32>([&](auto k) { scr[l + 32 * k] = v[k]; });
+    load(b, DB ? it + 2 : it + 1);
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kb = tid + j * NT, kp = (1024 - kb) & 1023;
+      cf zm[4], zmp[4], zr[4], zrp[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        zm[i] = slot(i)[kb]; zmp[i] = slot(i)[kp];
+        zr[i] = slot(4 + i)[kb]; zrp[i] = slot(4 + i)[kp];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        cf x0, x1;
+        split_pair2(zm[i], zmp[i], x0, x1);
+        const float tr = zr[i].x + zrp[i].x, ti = zr[i].y - zrp[i].y;
+        const float ir = zr[i].y + zrp[i].y, ii = zr[i].x - zrp[i].x;
+        const bool noise = ir * ir + ii * ii > tr * tr + ti * ti;
+        const float wgt = noise ? 1.0f : 0.0f;
+        bits[j] |= (noise ? 1u : 0u) << ((4 * it + i) & 31);
+        acc[j].add(x0, x1, wgt, wgt);
+      }
+    }
+    lds_barrier();
+  };
+  if constexpr (DB) {
+    for (int it = 0; it < iters; it += 2) {
+      step(ba, it);
+      step(bb, it + 1);
+    }
+  } else {
+    for (int it = 0; it < iters; ++it) step(ba, it);
+  }
+  float a = 0.f;
+  static_for<0, 2>([&](auto s) { a += acc[s].c00 + acc[s].c11 + acc[s].c01r + acc[s].c01i + acc[s].cm + (float)bits[s]; });
+  static_for<0, 32>([&](auto k) { a += v[k].x + v[k].y + ba[k] + (DB ? bb[k] : 0.f); });
+  out[blockIdx.x * NT + threadIdx.x] = a;
+}
+
 extern "C" int run_bench(int variant, const float* in, float* out, int blocks, int iters) {
   switch (variant) {
     case 0: { auto k = bench_x2<512>; int lds = 8 * 16896 + 8192;
@@ -310,6 +458,18 @@ extern "C" int run_bench(int variant, const float* in, float* out, int blocks, i
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
     case 9: { auto k = bench_x2_addtid<256>; int lds = 4 * 16896 + 8192;
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
+    case 20: case 21: {
+      auto k = variant == 20 ? bench_binphase_db<256, true> : bench_binphase_db<256, false>;
+      int lds = 4 * 16896 + 8192;
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
+    case 14: case 15: case 16: case 17: case 18: case 19: {
+      auto k = variant == 14 ? bench_binphase_loads<256, 1> : variant == 15 ? bench_binphase_loads<256, 2>
+             : variant == 16 ? bench_binphase_loads<256, 3> : variant == 17 ? bench_binphase_loads<256, 4>
+             : variant == 18 ? bench_binphase_loads<256, 5> : bench_binphase_loads<256, 6>;
+      int lds = 4 * 16896 + 8192;
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
     case 10: case 11: case 12: case 13: {

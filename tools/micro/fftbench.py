@@ -8,7 +8,7 @@ here = os.path.dirname(os.path.abspath(__file__))
 lib = ct.CDLL(os.path.join(here, "libfftbench.so"))
 lib.run_bench.argtypes = [ct.c_int, ct.c_void_p, ct.c_void_p, ct.c_int, ct.c_int]
 dev = torch.device("cuda")
-inp = torch.randn(1024, device=dev)
+inp = torch.randn(512 * 131072, device=dev)  # 256 MB: variants 14-16 stream from it
 out = torch.empty(1024 * 1024, device=dev)
 iters = 200
 names = {0: "x2 (32 pts/lane), 8 waves/block", 1: "x1 (16 pts/lane), 16 waves/block",
@@ -17,9 +17,13 @@ names = {0: "x2 (32 pts/lane), 8 waves/block", 1: "x1 (16 pts/lane), 16 waves/bl
          6: "x2 + wave-local LDS spectrum, 4 w/b", 7: "x2 arithmetic + LDS twiddles, no transpose",
          8: "x2 arithmetic only (no LDS at all)", 9: "x2 FFT only, addtid planar transpose",
          10: "pairs: FFT + in-register IBM bins, LDS tw", 11: "current: FFT + LDS bin phase, LDS tw",
-         12: "pairs, register twiddles", 13: "current, register twiddles"}
-ffts_per_block = {0: 16, 1: 16, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 8, 9: 8, 10: 8, 11: 8, 12: 8, 13: 8}
-for v, blocks in ((11, 512), (10, 512), (13, 512), (12, 512), (11, 512), (10, 512), (4, 512)):
+         12: "pairs, register twiddles", 13: "current, register twiddles",
+         14: "current + next-step loads (512 KB/block)", 15: "current + loads (16 KB/block, cached)",
+         16: "current + loads not feeding the FFT", 17: "current + dwordx2 loads (same bytes)",
+         18: "current + one channel's loads", 19: "current + 1/8 of the loads",
+         20: "LDS tw, one channel's loads, two steps ahead", 21: "LDS tw, one channel's loads, one step ahead"}
+ffts_per_block = {0: 16, 1: 16, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 8, 9: 8, 10: 8, 11: 8, 12: 8, 13: 8, 14: 8, 15: 8, 16: 8, 17: 8, 18: 8, 19: 8, 20: 8, 21: 8}
+for v, blocks in ((11, 512), (21, 512), (20, 512), (11, 512), (21, 512), (20, 512)):
     for _ in range(2):
         lib.run_bench(v, inp.data_ptr(), out.data_ptr(), blocks, iters)
     torch.cuda.synchronize()
