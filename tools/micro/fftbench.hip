@@ -443,6 +443,94 @@ __global__ void __launch_bounds__(NT, 2) bench_binphase_db(const float* in, floa
   out[blockIdx.x * NT + threadIdx.x] = a;
 }
 
+// Variant 22: the register-resident bin-pair layout (variant 12) fed by LDS-DMA: each
+// wave's 16.9 KB slot alternates between the raw samples of its next frame (mic pair
+// and reference pair, 4 x 4 KB, staged by 16 global_load_lds_dwordx4 issued right after
+// the transpose reads) and the transpose scratch. No sample VGPRs, no block barrier.
+template <int NT>
+__global__ void __launch_bounds__(NT, 2) bench_pairs_glds(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 5, l = lane & 31;
+  cf* tw = reinterpret_cast<cf*>(lds + (NT / 64) * 16896);
+  Fft1024x2::fill_twiddles(tw, threadIdx.x, NT);
+  Fft1024x2 f; f.init(lane);
+  unsigned char* wslot = lds + wave * 16896;
+  cf* scr = reinterpret_cast<cf*>(wslot + g * 8448);
+  constexpr int REGION = 131072;  // floats per block: four 32768-float streams
+  const float* src = in + (size_t)blockIdx.x * REGION;
+  auto dma = [&](int it) {  // the frame of step `it`: 4 streams x 1024 floats -> wslot
+    const int fr = it * 4 + wave;
+    const int off = (fr * 512) % (REGION / 4 - 1024);
+    static_for<0, 16>([&](auto q) {
+      constexpr int a = q / 4, part = q % 4;  // stream a, 1 KB part
+      const float* gp = src + a * (REGION / 4) + off + part * 256 + lane * 4;
+      __builtin_amdgcn_global_load_lds(gp, wslot + a * 4096 + part * 1024, 16, 0, 0);
+    });
+  };
+  dma(0);
+  __syncthreads();
+  __syncthreads();
+  const int lp = (32 - l) & 31;
+  const bool l0 = (l == 0);
+  Acc32 acc[8];
+  uint32_t bits[8];
+  static_for<0, 8>([&](auto s) { acc[s].zero(); bits[s] = 0u; });
+  cf v[32];
+  for (int it = 0; it < iters; ++it) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    {  // group 0: mic pair (streams 0, 1); group 1: reference pair (streams 2, 3)
+      const float* re = reinterpret_cast<const float*>(wslot + (2 * g) * 4096);
+      const float* im = re + 1024;
+      static_for<0, 32>([&](auto r) { v[r] = {re[l + 32 * r], im[l + 32 * r]}; });
+    }
+    __builtin_amdgcn_wave_barrier();
+    f.stage1(v, tw);
+    static_for<0, 32>([&](auto k) { scr[k * 33 + l] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    cf e[16], o[16];
+    static_for<0, 16>([&](auto n) {
+      const cf a = scr[l * 33 + n], b = scr[l * 33 + n + 16];
+      const cf c = scr[lp * 33 + n], d = scr[lp * 33 + n + 16];
+      e[n] = c_add(a, b);
+      o[n] = w32mul<n>(c_sub(c, d));
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (it + 1 < iters) dma(it + 1);
+    dft16(e);
+    dft16(o);
+    cf zk[16], zn[16];
+    static_for<0, 16>([&](auto s) {
+      if constexpr (s < 8) {
+        zk[s] = e[s];
+        const cf a = e[(16 - s) % 16], b = o[15 - s];
+        zn[s] = {l0 ? a.x : b.x, l0 ? a.y : b.y};
+      } else {
+        const cf a = o[s - 8], b = e[s];
+        zk[s] = {l0 ? a.x : b.x, l0 ? a.y : b.y};
+        const cf c = o[23 - s], d = o[15 - s];
+        zn[s] = {l0 ? c.x : d.x, l0 ? c.y : d.y};
+      }
+    });
+    static_for<0, 8>([&](auto s) { swap32(zk[s], zk[s + 8]); swap32(zn[s], zn[s + 8]); });
+    static_for<0, 8>([&](auto s) {
+      cf x0, x1;
+      split_pair2(zk[s], zn[s], x0, x1);
+      const cf zr = zk[s + 8], zrp = zn[s + 8];
+      const float tr = zr.x + zrp.x, ti = zr.y - zrp.y;
+      const float ir = zr.y + zrp.y, ii = zr.x - zrp.x;
+      const bool noise = ir * ir + ii * ii > tr * tr + ti * ti;
+      const float wgt = noise ? 1.0f : 0.0f;
+      bits[s] |= (noise ? 1u : 0u) << (it & 31);
+      acc[s].add(x0, x1, wgt, wgt);
+    });
+  }
+  float a = 0;
+  static_for<0, 8>([&](auto s) { a += acc[s].c00 + acc[s].c11 + acc[s].c01r + acc[s].c01i + acc[s].cm + (float)bits[s]; });
+  out[blockIdx.x * NT + threadIdx.x] = a;
+}
+
 extern "C" int run_bench(int variant, const float* in, float* out, int blocks, int iters) {
   switch (variant) {
     case 0: { auto k = bench_x2<512>; int lds = 8 * 16896 + 8192;
@@ -458,6 +546,11 @@ extern "C" int run_bench(int variant, const float* in, float* out, int blocks, i
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
     case 9: { auto k = bench_x2_addtid<256>; int lds = 4 * 16896 + 8192;
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
+    case 22: {
+      auto k = bench_pairs_glds<256>;
+      int lds = 4 * 16896 + 8192;
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
     case 20: case 21: {
