@@ -248,10 +248,11 @@ def main():
 
     K = args.steps
     if not args.no_kernel_timing:
-        plan.set_timing(True)
+        plan.set_timing(True, analysis_only=True)
     # No torch events inside the timed loop: a default torch.cuda.Event record is a
     # system-scope release (an L2 writeback, ~15 us between steps on MI355X); the plan's
-    # own per-kernel events are created with hipEventDisableSystemFence.
+    # own events are created with hipEventDisableSystemFence, and inside the timed region
+    # only the dominant (analysis) kernel is bracketed — five events per step cost 4-9 us.
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -264,7 +265,16 @@ def main():
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     step_ms = 1e3 * (t1 - t0) / K
-    kt = plan.timing() if not args.no_kernel_timing else None
+    kt = None
+    if not args.no_kernel_timing:
+        dom_timed = plan.timing()["analysis"]  # over the K timed steps
+        # every kernel of the chain: a separate, untimed pass with events around all four
+        plan.set_timing(True)
+        for _ in range(max(3, K // 4)):
+            step()
+        kt = plan.timing()
+        plan.set_timing(False)
+        kt["analysis_timed"] = dom_timed
     chain_ms = sum(kt[k] for k in plan.KERNELS) if kt else step_ms
 
     extra = {}
@@ -329,12 +339,13 @@ def main():
     if world > 1:
         dist.all_reduce(sums)
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        mx = torch.tensor([step_ms, chain_ms] + ([kt[k] for k in plan.KERNELS] if kt else []),
+        kn = plan.KERNELS + ("analysis_timed",)
+        mx = torch.tensor([step_ms, chain_ms] + ([kt[k] for k in kn] if kt else []),
                           dtype=torch.float64, device=dev)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         step_ms, chain_ms = float(mx[0]), float(mx[1])
         if kt:
-            kt.update({k: float(mx[2 + j]) for j, k in enumerate(plan.KERNELS)})
+            kt.update({k: float(mx[2 + j]) for j, k in enumerate(kn)})
     # SIR delta vs the reference restatement on identical inputs (rank 0, few utterances)
     d_sir = None
     if rank == 0 and args.workload != "unet":
@@ -364,14 +375,17 @@ def main():
             if not isinstance(traffic, dict):
                 traffic = {}
     if kt:
-        dom_ms = kt["analysis"]
+        dom_ms = kt["analysis_timed"]  # HIP events on the launch stream, over the timed steps
         roof = {"bound": "hbm", "achieved": alg_analysis / (dom_ms * 1e-3) / 1e9,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": alg_analysis / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "traffic": traffic.get("analysis"),
                 "kernel": info["kernel"], "kernel_ms": dom_ms,
                 "alg_bytes_per_launch": alg_analysis,
-                "kernels_ms": {k: kt[k] for k in plan.KERNELS},
+                "kernels_ms": {k: kt[k] for k in plan.KERNELS},  # separate untimed pass
+                "kernels_ms_note": "kernel_ms: analysis over the timed steps (two events "
+                                   "per step); kernels_ms/chain: all four kernels in an "
+                                   "untimed pass after them",
                 "chain": {"achieved": alg_chain / (chain_ms * 1e-3) / 1e9, "ms": chain_ms,
                           "alg_bytes_per_launch": alg_chain,
                           "frac": alg_chain / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,

@@ -121,10 +121,12 @@ int avz_plan_get_config(const avz_plan* plan, avz_config* cfg);
 int avz_num_frames(const avz_plan* plan, int len);
 int avz_mvdr_batch(const avz_plan* plan, const avz_batch_args* args, void* hip_stream);
 
-/* Diagnostics: record HIP events around the four kernels of every avz_mvdr_batch call
- * on this plan (analysis, solve, synthesis, finalize; enable != 0 also resets the
- * sums). avz_plan_get_timing waits for the outstanding calls and returns the average
- * milliseconds per kernel over the calls recorded since enabling. Not thread-safe. */
+/* Diagnostics: record HIP events around the kernels of every avz_mvdr_batch call on
+ * this plan: enable 1 = all four (analysis, solve, synthesis, finalize), 2 = the analysis
+ * kernel only (two events per call), 0 = off; enabling also resets the sums.
+ * avz_plan_get_timing waits for the outstanding calls and returns the average
+ * milliseconds per kernel over the calls recorded since enabling (NaN for kernels not
+ * timed). Not thread-safe. */
 int avz_plan_set_timing(avz_plan* plan, int enable);
 int avz_plan_get_timing(avz_plan* plan, double* ms_avg /*[4]*/, int* calls);
 

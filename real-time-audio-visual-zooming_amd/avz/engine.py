@@ -105,12 +105,15 @@ class MVDRPlan:
     # ------------------------------------------------------------------ diagnostics
     KERNELS = ("analysis", "solve", "synthesis", "finalize")
 
-    def set_timing(self, enable: bool = True) -> None:
-        """Record HIP events around each of the chain's four kernels on every run()."""
-        check(lib.avz_plan_set_timing(self._h, int(enable)), "avz_plan_set_timing")
+    def set_timing(self, enable: bool = True, analysis_only: bool = False) -> None:
+        """Record HIP events around each of the chain's four kernels on every run()
+        (analysis_only: around the analysis kernel alone, two events per run)."""
+        mode = (2 if analysis_only else 1) if enable else 0
+        check(lib.avz_plan_set_timing(self._h, mode), "avz_plan_set_timing")
 
     def timing(self) -> dict:
-        """Average ms per kernel over the runs since set_timing(True) (waits for them)."""
+        """Average ms per kernel over the runs since set_timing(True) (waits for them;
+        NaN for kernels not timed)."""
         ms = (ct.c_double * 4)()
         n = ct.c_int()
         check(lib.avz_plan_get_timing(self._h, ms, ct.byref(n)), "avz_plan_get_timing")

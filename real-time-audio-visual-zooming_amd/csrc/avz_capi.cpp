@@ -3,6 +3,7 @@
 
 #include <cmath>
 #include <complex>
+#include <limits>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -29,6 +30,7 @@ struct avz_plan {
   float* pf_gain;            // [max_batch][nchunk][32][F] IRM gains (AVZ_PF_IRM plans only)
   // diagnostic per-kernel timing (avz_plan_set_timing): two event sets used alternately
   bool timing;
+  int n_ev;  // events recorded per call: 5 (all four kernels) or 2 (analysis only)
   hipEvent_t ev[2][5];
   bool ev_pending[2];
   int ev_next;
@@ -39,8 +41,8 @@ struct avz_plan {
 static void timing_drain(avz_plan* p, int set) {
   if (!p->ev_pending[set]) return;
   p->ev_pending[set] = false;
-  if (hipEventSynchronize(p->ev[set][4]) != hipSuccess) return;
-  for (int i = 0; i < 4; ++i) {
+  if (hipEventSynchronize(p->ev[set][p->n_ev - 1]) != hipSuccess) return;
+  for (int i = 0; i < p->n_ev - 1; ++i) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, p->ev[set][i], p->ev[set][i + 1]) == hipSuccess) p->ms_sum[i] += ms;
   }
@@ -259,6 +261,7 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
     timing_drain(mp, set);  // the call two back: the previous call keeps the GPU busy
     for (int i = 0; i < 5; ++i) evs[i] = mp->ev[set][i];
     k.events = evs;
+    k.n_events = mp->n_ev;
   }
   k.beamformer = c.beamformer;
   k.bypass_hz = c.bypass_hz;
@@ -277,6 +280,8 @@ extern "C" int avz_plan_set_timing(avz_plan* p, int enable) {
   p->ms_calls = 0;
   for (double& m : p->ms_sum) m = 0.0;
   if (!enable) return AVZ_OK;
+  if (enable != 1 && enable != 2) return AVZ_ERR_ARG;
+  p->n_ev = enable == 2 ? 2 : 5;
   for (int s = 0; s < 2; ++s)
     for (int i = 0; i < 5; ++i) {
       const hipError_t e = hipEventCreateWithFlags(&p->ev[s][i], hipEventDisableSystemFence);
@@ -295,7 +300,9 @@ extern "C" int avz_plan_get_timing(avz_plan* p, double* ms_avg, int* calls) {
   if (!p->timing) return AVZ_ERR_ARG;
   timing_drain(p, p->ev_next);
   timing_drain(p, p->ev_next ^ 1);
-  for (int i = 0; i < 4; ++i) ms_avg[i] = p->ms_calls ? p->ms_sum[i] / p->ms_calls : 0.0;
+  for (int i = 0; i < 4; ++i)
+    ms_avg[i] = i >= p->n_ev - 1 ? std::numeric_limits<double>::quiet_NaN()
+                                 : (p->ms_calls ? p->ms_sum[i] / p->ms_calls : 0.0);
   if (calls) *calls = p->ms_calls;
   return AVZ_OK;
 }

@@ -860,7 +860,7 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
   hipEvent_t const* ev = reinterpret_cast<hipEvent_t const*>(a->events);
   auto mark = [&](int i) {
-    if (ev) (void)hipEventRecord(ev[i], st);
+    if (ev && i < a->n_events) (void)hipEventRecord(ev[i], st);
   };
   mark(0);
   hipLaunchKernelGGL(k1, pgrid, dim3(kCThreads), lds, st, *a);

@@ -46,6 +46,7 @@ struct ChainArgs {
   float* pf_gain;             // [B][nchunk][32][F] IRM post-filter gain (PF_IRM) or null
   int singular_fallback;      // 0: w = [1, 0]; 1: w = [1/2, 1/2]
   void* const* events;        // host-only: 5 hipEvent_t recorded around the 4 launches, or null
+  int n_events;               // host-only: how many of them to record (5, or 2: analysis only)
 };
 
 struct StftArgs {

@@ -130,3 +130,31 @@ def test_batch_run_gpu_matches_oracle_enhancer(gpu_device):
                               enhance=oracle_enhance)
     assert gpu.sums[4] == 6
     np.testing.assert_allclose(gpu.sums[:4] / 6, ref.sums[:4] / 6, atol=0.01)  # mean dB
+
+
+def test_plan_timing_modes(gpu_device):
+    """avz_plan_set_timing: mode 1 times all four kernels, mode 2 the analysis kernel
+    only (NaN for the rest), 0 turns it off (get_timing then reports an argument error)."""
+    import math
+
+    import avz
+    from avz._lib import AvzError
+    from avz import synth
+    mix, tgt, itf = synth.make_batch(4, n_samples=32000)
+    d = [torch.from_numpy(x).to(gpu_device) for x in (mix, tgt, itf)]
+    plan = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
+                        max_batch=4, max_samples=32000)
+    for mode in ("all", "analysis"):
+        plan.set_timing(True, analysis_only=(mode == "analysis"))
+        for _ in range(3):
+            plan.run(d[0], ref_tgt=d[1], ref_int=d[2])
+        t = plan.timing()
+        assert t["calls"] == 3 and t["analysis"] > 0
+        others = [t[k] for k in ("solve", "synthesis", "finalize")]
+        if mode == "all":
+            assert all(v > 0 for v in others)
+        else:
+            assert all(math.isnan(v) for v in others)
+    plan.set_timing(False)
+    with pytest.raises(AvzError):
+        plan.timing()
