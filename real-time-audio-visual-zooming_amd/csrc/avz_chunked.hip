@@ -246,8 +246,11 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     uint32_t ipd_fix[BPT];
 #pragma unroll
     for (int j = 0; j < BPT; ++j) ipd_fix[j] = 0u;
-    auto bin_phase = [&](auto full) {
-      // frames whose reads are batched together (IPD: one, its inlined atan2f fallback is big)
+    const bool mask_vec = MASK == MASK_EXTERNAL && A.mask_st == 1 && (A.mask_sf & 3) == 0 &&
+                          (A.mask_sb & 3) == 0 &&
+                          ((reinterpret_cast<uintptr_t>(A.ext_mask) & 15) == 0) && (f0 & 3) == 0;
+    auto bin_phase = [&](auto full, auto vec) {
+      // frames whose LDS reads are batched together
       constexpr int G = FB < 4 ? FB : 4;
 #pragma unroll
       for (int j = 0; j < BPT; ++j) {
@@ -255,6 +258,17 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         const int kp = (N - kb) & (N - 1);
 #pragma unroll
         for (int g0 = 0; g0 < FB; g0 += G) {
+          // External mask with t-contiguous, 16-B aligned rows: the bin's G mask values
+          // of a full step in one 16-B load (as the synthesis post-filter).
+          float mv[MASK == MASK_EXTERNAL ? 4 : 1];
+          if constexpr (MASK == MASK_EXTERNAL && G == 4 && decltype(vec)::value) {
+            const float4 m4 = *reinterpret_cast<const float4*>(
+                A.ext_mask + (long long)b * A.mask_sb + (long long)kb * A.mask_sf + f0 + g0);
+            mv[0] = m4.x;
+            mv[1] = m4.y;
+            mv[2] = m4.z;
+            mv[3] = m4.w;
+          }
           cf zm[G], zmp[G], zr[G], zrp[G];
 #pragma unroll
           for (int i = 0; i < G; ++i) {
@@ -284,8 +298,13 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
               }
               bool noise = false;
               float wgt;
-              const float m =
-                  bin_mask<MASK>(A, b, x0, x1, zr[i], zrp[i], kb, f0 + g0 + i, noise, wgt);
+              float m;
+              if constexpr (MASK == MASK_EXTERNAL && G == 4 && decltype(vec)::value) {
+                m = 1.0f - mv[i];
+                wgt = m + A.weight_eps;
+              } else {
+                m = bin_mask<MASK>(A, b, x0, x1, zr[i], zrp[i], kb, f0 + g0 + i, noise, wgt);
+              }
               bits[j] |= (noise ? 1u : 0u) << (step * FB + g0 + i);
               acc[j].add(x0, x1, wgt, m);
               if constexpr (IRM) gain[(step * FB + g0 + i) * F + kb] = irm_gain(zr[i], zrp[i]);
@@ -294,10 +313,18 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         }
       }
     };
-    if (nvalid == FB)
-      bin_phase(std::true_type{});
-    else
-      bin_phase(std::false_type{});
+    if (nvalid == FB) {
+      if constexpr (MASK == MASK_EXTERNAL) {
+        if (mask_vec)
+          bin_phase(std::true_type{}, std::true_type{});
+        else
+          bin_phase(std::true_type{}, std::false_type{});
+      } else {
+        bin_phase(std::true_type{}, std::false_type{});
+      }
+    } else {
+      bin_phase(std::false_type{}, std::false_type{});
+    }
     if constexpr (MASK == MASK_IPD) {
       // Near-colinear (bin, frame) pairs (always DC, rarely any other): exact weight from
       // the spectra still in LDS. Waves with no such lane skip this.
@@ -574,6 +601,9 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   }
   const float* irm = (PF == PF_IRM) ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F
                                     : nullptr;
+  const bool mask_vec = (PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) && A.mask_st == 1 &&
+                        (A.mask_sf & 3) == 0 && (A.mask_sb & 3) == 0 &&
+                        ((reinterpret_cast<uintptr_t>(A.ext_mask) & 15) == 0);
   auto gain = [&](uint32_t bb, int i, int t, int k) -> float {  // i: frame bit in chunk
     if (t >= T) return 0.0f;
     if constexpr (PF == PF_IBM_TARGET) {
@@ -622,6 +652,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     AVZ_STAMP(6);
 
     // ---- apply w^H y and the post-filter; pack frames (2p, 2p+1) into slot 2p
+    auto apply_phase = [&](auto vec) {
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
       const int kb = tid + j * NT;
@@ -638,18 +669,53 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         zb[p] = Zb[kb];
         zbp[p] = Zb[kp];
       }
+      // External mask with t-contiguous, 16-B aligned rows (the U-Net / TFLite outputs):
+      // the bin's FB gains of this step in FB/4 16-B loads instead of FB scattered ones.
+      constexpr bool VEC = decltype(vec)::value;
+      float gv[VEC ? FB : 1];
+      if constexpr (VEC) {
+        const float4* mp = reinterpret_cast<const float4*>(
+            A.ext_mask + (long long)b * A.mask_sb + (long long)kb * A.mask_sf + f0);
+#pragma unroll
+        for (int q = 0; q < FB / 4; ++q) {
+          const float4 m = mp[q];
+          gv[4 * q + 0] = m.x;
+          gv[4 * q + 1] = m.y;
+          gv[4 * q + 2] = m.z;
+          gv[4 * q + 3] = m.w;
+        }
+#pragma unroll
+        for (int i = 0; i < FB; ++i)
+          if constexpr (PF == PF_EXT_FLOOR) gv[i] = fmaxf(gv[i], A.pf_floor);
+      }
 #pragma unroll
       for (int p = 0; p < NPAIR; ++p) {
         const int ta = f0 + 2 * p;
         cf* Za = slot_ptr<N>(lds, 2 * p);
         const int ia = step * FB + 2 * p;
-        const float ga = gain(bits[j], ia, ta, kb), gb = gain(bits[j], ia + 1, ta + 1, kb);
+        float ga, gb;
+        if constexpr (VEC) {
+          ga = gv[2 * p];
+          gb = gv[2 * p + 1];
+        } else {
+          ga = gain(bits[j], ia, ta, kb);
+          gb = gain(bits[j], ia + 1, ta + 1, kb);
+        }
         const cf sa = apply_bin(alpha[j], beta[j], za[p], zap[p], ga);
         const cf sb = apply_bin(alpha[j], beta[j], zb[p], zbp[p], gb);
         Za[kp] = {sa.x + sb.y, sb.x - sa.y};  // conj(Sa) + i conj(Sb) at N - k
         // Sa + i Sb at k; at DC irfft keeps only the real parts (written last: kp == kb)
         Za[kb] = (kb == 0) ? cf{sa.x, sb.x} : cf{sa.x - sb.y, sa.y + sb.x};
       }
+    }
+    };
+    if constexpr (PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) {
+      if (mask_vec && f0 + FB <= T)  // wave-uniform
+        apply_phase(std::true_type{});
+      else
+        apply_phase(std::false_type{});
+    } else {
+      apply_phase(std::false_type{});
     }
     if (nyq_wave && lane < NPAIR) {  // Nyquist bin: frame pair `lane`
       const int ta = f0 + 2 * lane;
