@@ -167,6 +167,12 @@ def test_fused_external_mask(avz, gpu_device, n, floor):
     scale = np.max(np.abs(ref))
     assert np.max(np.abs(got - ref)) <= WAVE_TOL * scale
     assert abs(float(peak[0]) - scale) <= 1e-4 * scale
+    # the same mask as a transposed (bin-contiguous) view: the kernels' strided path
+    Mt = dev_t(np.ascontiguousarray(M.T), gpu_device).t()
+    out2, _ = plan.run(dev_t(mix, gpu_device)[None], ext_mask=Mt[None])
+    torch.cuda.synchronize()
+    got2 = out2[0, :len(ref)].cpu().numpy()
+    assert np.max(np.abs(got2 - ref)) <= WAVE_TOL * scale
 
 
 # ----------------------------------------------------------------------------- batching
