@@ -13,7 +13,17 @@
  *    throws across the ABI (the reference reports errors by print-and-return,
  *    e.g. oracle_debug.py:31-33; singular solves fall back to w = [1, 0],
  *    oracle_debug.py:78-79 — the kernels reproduce that fallback per bin).
- *  - A plan is immutable after creation and may be used from several streams.
+ *  - A plan's configuration and steering table are immutable after creation. Every
+ *    avz_mvdr_batch call needs a per-call device workspace (chunk partials, mask words,
+ *    apply coefficients, seam halves, peak words). A call that passes its own
+ *    (avz_batch_args.workspace, sized by avz_mvdr_workspace_bytes) shares nothing
+ *    mutable with other calls, so calls with distinct workspaces may run concurrently
+ *    on different streams. A call that passes workspace = NULL uses the plan's own
+ *    workspace: such calls (and avz_srp_scan, which always uses it) must be ordered
+ *    on one stream or otherwise serialised by the caller. The diagnostic timing state
+ *    (avz_plan_set_timing) is not thread-safe.
+ *  - Device lengths len[b] are clamped to the call's host-validated max_len in every
+ *    kernel, so an inconsistent len[] cannot move an access outside the caller's rows.
  */
 #ifndef AVZ_H_
 #define AVZ_H_
@@ -112,6 +122,10 @@ typedef struct avz_batch_args {
   double* cov_out;         /* debug: [batch][F][5] sum m|y0|^2, sum m|y1|^2, Re/Im sum m y0 y1*,
                               sum m   (or NULL)                                                  */
   float* w_out;            /* debug: [batch][F][4] Re w0, Im w0, Re w1, Im w1 (or NULL)         */
+  int mask_bins;           /* EXTERNAL: bins of ext_mask (>= F) and frames (>= frames of max_len) */
+  int mask_frames;
+  void* workspace;         /* per-call device workspace (256-byte aligned), or NULL: the plan's */
+  long long workspace_bytes; /* >= avz_mvdr_workspace_bytes(plan, batch, max_len)              */
 } avz_batch_args;
 
 int avz_plan_create(avz_plan** plan, const avz_config* cfg);
@@ -120,6 +134,9 @@ int avz_plan_get_config(const avz_plan* plan, avz_config* cfg);
 /* Frames of an utterance of len samples: ceil(len/hop) + 1 (scipy padded/boundary). */
 int avz_num_frames(const avz_plan* plan, int len);
 int avz_mvdr_batch(const avz_plan* plan, const avz_batch_args* args, void* hip_stream);
+/* Device bytes of a per-call workspace for `batch` utterances of at most max_len samples
+ * (negative AVZ_ERR_* on bad arguments). */
+long long avz_mvdr_workspace_bytes(const avz_plan* plan, int batch, int max_len);
 
 /* Diagnostics: record HIP events around the kernels of every avz_mvdr_batch call on
  * this plan: enable 1 = all four (analysis, solve, synthesis, finalize), 2 = the analysis

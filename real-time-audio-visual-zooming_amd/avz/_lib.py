@@ -36,7 +36,7 @@ EXPORTED = [
     "avz_mvdr_batch", "avz_plan_set_timing", "avz_plan_get_timing", "avz_stft",
     "avz_chunk_split", "avz_chunk_merge", "avz_mask_features", "avz_srp_scan",
     "avz_projection_metrics", "avz_scene_workspace_bytes", "avz_scene_mix", "avz_strerror",
-    "avz_last_hip_error", "avz_version",
+    "avz_last_hip_error", "avz_version", "avz_mvdr_workspace_bytes",
 ]
 
 
@@ -63,6 +63,8 @@ class AvzBatchArgs(ct.Structure):
         ("mask_stride_f", ct.c_longlong), ("mask_stride_t", ct.c_longlong),
         ("out", ct.c_void_p), ("out_stride", ct.c_longlong), ("peak", ct.c_void_p),
         ("cov_out", ct.c_void_p), ("w_out", ct.c_void_p),
+        ("mask_bins", ct.c_int), ("mask_frames", ct.c_int),
+        ("workspace", ct.c_void_p), ("workspace_bytes", ct.c_longlong),
     ]
 
 
@@ -97,6 +99,8 @@ def _load():
     lib.avz_plan_get_config.argtypes = [P, ct.POINTER(AvzConfig)]
     lib.avz_num_frames.argtypes = [P, ct.c_int]
     lib.avz_mvdr_batch.argtypes = [P, ct.POINTER(AvzBatchArgs), P]
+    lib.avz_mvdr_workspace_bytes.argtypes = [P, ct.c_int, ct.c_int]
+    lib.avz_mvdr_workspace_bytes.restype = ct.c_longlong
     lib.avz_stft.argtypes = [P, ct.c_int, ct.c_int, P, ct.c_int, P, ct.c_longlong, ct.c_longlong,
                              P, ct.c_longlong, ct.c_longlong, ct.c_longlong, P]
     I, LL = ct.c_int, ct.c_longlong

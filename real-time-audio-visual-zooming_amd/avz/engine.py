@@ -131,12 +131,24 @@ class MVDRPlan:
         return torch.empty((batch, (n + 3) // 4 * 4), dtype=torch.float32, device=device)
 
     # ------------------------------------------------------------------ batch call
+    def workspace_bytes(self, batch: int, max_len: int) -> int:
+        """Device bytes of a per-call workspace (avz_mvdr_workspace_bytes)."""
+        return check(lib.avz_mvdr_workspace_bytes(self._h, int(batch), int(max_len)),
+                     "avz_mvdr_workspace_bytes")
+
+    def alloc_workspace(self, batch: int, max_len: int, device) -> torch.Tensor:
+        """A per-call workspace: calls given distinct workspaces may overlap on different
+        streams (include/avz.h); calls without one share the plan's and must not."""
+        n = self.workspace_bytes(batch, max_len)
+        return torch.empty((max(n, 1) + 255) // 256 * 256, dtype=torch.uint8, device=device)
+
     def run(self, mix: torch.Tensor, lengths: torch.Tensor | None = None, *,
             max_len: int | None = None, ref_tgt=None, ref_int=None, ext_mask=None,
             out: torch.Tensor | None = None, peak: torch.Tensor | None = None,
-            cov_out=None, w_out=None, stream=None):
+            cov_out=None, w_out=None, workspace: torch.Tensor | None = None, stream=None):
         """mix: [B, 2, S] float32 (device); lengths: [B] int32 (device, default S).
         ref_tgt/ref_int: [B, S] (IBM); ext_mask: [B, F, T] target probability (EXTERNAL).
+        workspace: optional uint8 device tensor of >= workspace_bytes(B, max_len) bytes.
         Returns (out [B, >= out_len], peak [B])."""
         if not mix.is_cuda:
             raise ValueError("mix must be a device tensor")
@@ -149,14 +161,23 @@ class MVDRPlan:
         if lengths is None:
             lengths = torch.full((B,), S, dtype=torch.int32, device=dev)
             max_len = S
+        if lengths.dtype != torch.int32 or not lengths.is_cuda or lengths.dim() != 1 \
+                or lengths.shape[0] < B:
+            raise ValueError("lengths must be an int32 device tensor of >= B entries")
         if max_len is None:
-            max_len = int(lengths.max().item())
-        if lengths.dtype != torch.int32 or not lengths.is_cuda:
-            raise ValueError("lengths must be an int32 device tensor")
+            max_len = int(lengths[:B].max().item())
+        if max_len > S:
+            raise ValueError(f"max_len {max_len} exceeds the {S} samples of mix")
+        T = self.frames(max_len)
         if out is None:
             out = self.alloc_out(B, max_len, dev)
         if peak is None:
             peak = torch.empty((B,), dtype=torch.float32, device=dev)
+        if out.dtype != torch.float32 or out.dim() != 2 or out.shape[0] < B or \
+                out.shape[1] < self.out_len(max_len) or out.stride(1) != 1:
+            raise ValueError("out must be float32 [>= B, >= out_len(max_len)]")
+        if peak.dtype != torch.float32 or peak.numel() < B or not peak.is_contiguous():
+            raise ValueError("peak must be a contiguous float32 tensor of >= B entries")
         a = AvzBatchArgs()
         a.batch = B
         a.len = lengths.data_ptr()
@@ -165,8 +186,9 @@ class MVDRPlan:
         a.mix_stride = mix.stride(0)
         a.ch_stride = mix.stride(1)
         for r in (ref_tgt, ref_int):
-            if r is not None and (r.dtype != torch.float32 or r.stride(-1) != 1 or not r.is_cuda):
-                raise ValueError("references must be float32 device tensors [B, S]")
+            if r is not None and (r.dtype != torch.float32 or r.stride(-1) != 1 or not r.is_cuda
+                                  or r.dim() != 2 or r.shape[0] < B or r.shape[1] < max_len):
+                raise ValueError("references must be float32 device tensors [B, >= max_len]")
         if ref_tgt is not None:
             a.ref_tgt = ref_tgt.data_ptr()
             a.ref_stride = ref_tgt.stride(0)
@@ -177,13 +199,22 @@ class MVDRPlan:
         if ext_mask is not None:
             if ext_mask.dtype != torch.float32 or not ext_mask.is_cuda or ext_mask.dim() != 3:
                 raise ValueError("ext_mask must be float32 [B, F, T] on the device")
+            if ext_mask.shape[0] < B or ext_mask.shape[1] < self.F or ext_mask.shape[2] < T:
+                raise ValueError(f"ext_mask {tuple(ext_mask.shape)} does not cover "
+                                 f"[B={B}, F={self.F}, T={T}]")
             a.ext_mask = ext_mask.data_ptr()
             a.mask_stride_b, a.mask_stride_f, a.mask_stride_t = ext_mask.stride()
+            a.mask_bins, a.mask_frames = ext_mask.shape[1], ext_mask.shape[2]
         a.out = out.data_ptr()
         a.out_stride = out.stride(0)
         a.peak = peak.data_ptr()
         a.cov_out = 0 if cov_out is None else cov_out.data_ptr()
         a.w_out = 0 if w_out is None else w_out.data_ptr()
+        if workspace is not None:
+            if workspace.dtype != torch.uint8 or not workspace.is_cuda:
+                raise ValueError("workspace must be a uint8 device tensor")
+            a.workspace = workspace.data_ptr()
+            a.workspace_bytes = workspace.numel()
         check(lib.avz_mvdr_batch(self._h, ct.byref(a), _stream_handle(stream)), "avz_mvdr_batch")
         return out, peak
 

@@ -13,21 +13,53 @@
 #include "../../include/avz.h"
 #include "avz_internal.h"
 
+// Per-call device workspace of the chain (see avz_internal.h ChainArgs), carved from one
+// caller-provided block (avz_mvdr_workspace_bytes) or from the plan's own arena.
+struct Workspace {
+  float* part;
+  uint32_t* mwords;
+  float* coef;               // [batch][F][4] per-bin apply coefficients
+  float* heads;
+  float* tails;
+  uint32_t* peak_u;
+  float* pf_gain;            // [batch][nchunk][32][F] IRM gains (AVZ_PF_IRM plans only)
+};
+
+static size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
+
+// Bytes of a workspace for `batch` utterances of at most `nchunk` 32-frame chunks; with a
+// non-null base also carves it into *w. Every piece starts on a 256-byte boundary.
+static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* base, Workspace* w) {
+  const int F = c.n_fft / 2 + 1, H = c.n_fft / 2, CF = avz_chunk_frames();
+  const long long B = batch;
+  const size_t sz_part = align256(sizeof(float) * B * nchunk * 5 * F);
+  const size_t sz_mw = align256(sizeof(uint32_t) * B * nchunk * F);
+  const size_t sz_coef = align256(sizeof(float) * B * F * 4);
+  const size_t sz_ht = align256(sizeof(float) * B * nchunk * H);
+  const size_t sz_b = align256(sizeof(uint32_t) * B);
+  const size_t sz_gain =
+      c.postfilter == AVZ_PF_IRM ? align256(sizeof(float) * B * nchunk * CF * F) : 0;
+  if (base && w) {
+    char* q = base;
+    w->part = reinterpret_cast<float*>(q); q += sz_part;
+    w->mwords = reinterpret_cast<uint32_t*>(q); q += sz_mw;
+    w->coef = reinterpret_cast<float*>(q); q += sz_coef;
+    w->heads = reinterpret_cast<float*>(q); q += sz_ht;
+    w->tails = reinterpret_cast<float*>(q); q += sz_ht;
+    w->peak_u = reinterpret_cast<uint32_t*>(q); q += sz_b;
+    w->pf_gain = sz_gain ? reinterpret_cast<float*>(q) : nullptr;
+  }
+  return sz_part + sz_mw + sz_coef + 2 * sz_ht + sz_b + sz_gain;
+}
+
 struct avz_plan {
   avz_config cfg;
   double tau1, tau2;         // far-field delays of the two mics (masked_mvdr.py:28-29)
   int max_frames;
-  // chunked path workspace, one allocation (see avz_internal.h ChainArgs)
-  int nchunk;
-  void* arena;
-  float* part;
-  uint32_t* mwords;
+  int nchunk;                // 32-frame chunks of a max_samples utterance
+  void* arena;               // steering table + the plan's own workspace
   double* steer;             // [F][4] steering vectors (masked_mvdr.py:22-35), fp64
-  float* coef;               // [max_batch][F][4] per-bin apply coefficients
-  float* heads;
-  float* tails;
-  uint32_t* peak_u;
-  float* pf_gain;            // [max_batch][nchunk][32][F] IRM gains (AVZ_PF_IRM plans only)
+  Workspace ws;              // used by calls that pass no workspace (serialised by contract)
   // diagnostic per-kernel timing (avz_plan_set_timing): two event sets used alternately
   bool timing;
   int n_ev;  // events recorded per call: 5 (all four kernels) or 2 (analysis only)
@@ -63,7 +95,7 @@ static int hip_fail(hipError_t e) {
   return AVZ_ERR_HIP;
 }
 
-extern "C" int avz_version(void) { return 1; }
+extern "C" int avz_version(void) { return 2; }
 
 extern "C" const char* avz_last_hip_error(void) { return g_last_hip.c_str(); }
 
@@ -114,34 +146,17 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
   p->max_frames = frames_for(c.max_samples, c.hop);
   const int F = c.n_fft / 2 + 1;
   {
-    const int H = c.n_fft / 2;
-    const long long B = c.max_batch;
     p->nchunk = (p->max_frames + avz_chunk_frames() - 1) / avz_chunk_frames();
-    auto up = [](size_t n) { return (n + 255) & ~size_t(255); };
-    const size_t sz_part = up(sizeof(float) * B * p->nchunk * 5 * F);
-    const size_t sz_mw = up(sizeof(uint32_t) * B * p->nchunk * F);
-    const size_t sz_steer = up(sizeof(double) * F * 4);
-    const size_t sz_coef = up(sizeof(float) * B * F * 4);
-    const size_t sz_ht = up(sizeof(float) * B * p->nchunk * H);
-    const size_t sz_b = up(sizeof(uint32_t) * B);
-    const size_t sz_gain = c.postfilter == AVZ_PF_IRM
-                               ? up(sizeof(float) * B * p->nchunk * avz_chunk_frames() * F)
-                               : 0;
-    hipError_t e =
-        hipMalloc(&p->arena, sz_part + sz_mw + sz_steer + sz_coef + 2 * sz_ht + sz_b + sz_gain);
+    const size_t sz_steer = align256(sizeof(double) * F * 4);
+    const size_t sz_ws = ws_layout(c, c.max_batch, p->nchunk, nullptr, nullptr);
+    hipError_t e = hipMalloc(&p->arena, sz_steer + sz_ws);
     if (e != hipSuccess) {
       delete p;
       return hip_fail(e);
     }
     char* q = static_cast<char*>(p->arena);
-    p->part = reinterpret_cast<float*>(q); q += sz_part;
-    p->mwords = reinterpret_cast<uint32_t*>(q); q += sz_mw;
-    p->steer = reinterpret_cast<double*>(q); q += sz_steer;
-    p->coef = reinterpret_cast<float*>(q); q += sz_coef;
-    p->heads = reinterpret_cast<float*>(q); q += sz_ht;
-    p->tails = reinterpret_cast<float*>(q); q += sz_ht;
-    p->peak_u = reinterpret_cast<uint32_t*>(q); q += sz_b;
-    p->pf_gain = sz_gain ? reinterpret_cast<float*>(q) : nullptr;
+    p->steer = reinterpret_cast<double*>(q);
+    ws_layout(c, c.max_batch, p->nchunk, q + sz_steer, &p->ws);
     // d_m(f_k) = exp(-1j * (2 pi f_k) * tau_m), f_k = np.fft.rfftfreq(n_fft, 1/fs)[k]
     // (masked_mvdr.py:22-35); the hybrid null beamformer phase-normalises it to mic 0,
     // v / (v[0] + 1e-10) (Final_pipeline/src/inference.py:16-26).
@@ -192,6 +207,16 @@ extern "C" int avz_num_frames(const avz_plan* p, int len) {
   return frames_for(len, p->cfg.hop);
 }
 
+static int chunks_for(int max_len, int hop) {
+  return (frames_for(max_len, hop) + avz_chunk_frames() - 1) / avz_chunk_frames();
+}
+
+extern "C" long long avz_mvdr_workspace_bytes(const avz_plan* p, int batch, int max_len) {
+  if (!p || batch < 0 || batch > p->cfg.max_batch) return AVZ_ERR_SHAPE;
+  if (max_len < p->cfg.n_fft || max_len > p->cfg.max_samples) return AVZ_ERR_SHAPE;
+  return (long long)ws_layout(p->cfg, batch, chunks_for(max_len, p->cfg.hop), nullptr, nullptr);
+}
+
 extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* stream) {
   if (!p || !a) return AVZ_ERR_ARG;
   const avz_config& c = p->cfg;
@@ -202,6 +227,7 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   if (a->ch_stride < a->max_len) return AVZ_ERR_SHAPE;
   if (a->batch > 1 && a->mix_stride < a->ch_stride + a->max_len) return AVZ_ERR_SHAPE;
   const int T = frames_for(a->max_len, c.hop);
+  const int F = c.n_fft / 2 + 1;
   const long long out_len = (long long)(T - 1) * c.hop;
   if (a->batch > 1 && a->out_stride < out_len) return AVZ_ERR_SHAPE;
   if ((a->out_stride & 3) || (reinterpret_cast<uintptr_t>(a->out) & 15)) return AVZ_ERR_ALIGN;
@@ -209,11 +235,25 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
     if (!a->ref_tgt || !a->ref_int) return AVZ_ERR_ARG;
     if (a->batch > 1 && a->ref_stride < a->max_len) return AVZ_ERR_SHAPE;
   }
-  if (c.mask_mode == AVZ_MASK_EXTERNAL && !a->ext_mask) return AVZ_ERR_ARG;
+  if (c.mask_mode == AVZ_MASK_EXTERNAL) {
+    if (!a->ext_mask) return AVZ_ERR_ARG;
+    // the kernels read M[b][k][t] for every bin and every frame of the longest utterance
+    if (a->mask_bins < F || a->mask_frames < T) return AVZ_ERR_SHAPE;
+  }
+  Workspace ws = p->ws;
+  int nchunk = p->nchunk;
+  if (a->workspace) {
+    nchunk = chunks_for(a->max_len, c.hop);
+    if (reinterpret_cast<uintptr_t>(a->workspace) & 255) return AVZ_ERR_ALIGN;
+    if (a->workspace_bytes < (long long)ws_layout(c, a->batch, nchunk, nullptr, nullptr))
+      return AVZ_ERR_SHAPE;
+    ws_layout(c, a->batch, nchunk, static_cast<char*>(a->workspace), &ws);
+  }
 
   avz::ChainArgs k{};
   k.batch = a->batch;
   k.len = a->len;
+  k.max_len = a->max_len;
   k.mix = a->mix;
   k.mix_stride = a->mix_stride;
   k.ch_stride = a->ch_stride;
@@ -242,17 +282,17 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   k.postfilter = c.postfilter;
   k.normalize = c.normalize;
   k.max_frames = T;
-  k.nchunk = p->nchunk;
-  k.part = p->part;
-  k.mwords = p->mwords;
+  k.nchunk = nchunk;
+  k.part = ws.part;
+  k.mwords = ws.mwords;
   k.steer = p->steer;
-  k.coef = p->coef;
-  k.heads = p->heads;
-  k.tails = p->tails;
-  k.peak_u = p->peak_u;
-  k.pf_gain = p->pf_gain;
+  k.coef = ws.coef;
+  k.heads = ws.heads;
+  k.tails = ws.tails;
+  k.peak_u = ws.peak_u;
+  k.pf_gain = ws.pf_gain;
   k.singular_fallback = c.singular_fallback;
-  avz_plan* mp = const_cast<avz_plan*>(p);  // timing state only (diagnostic)
+  avz_plan* mp = const_cast<avz_plan*>(p);  // diagnostic timing state only (not thread-safe)
   void* evs[5];
   int set = -1;
   if (mp->timing) {
@@ -330,6 +370,7 @@ extern "C" int avz_stft(const avz_plan* p, int batch, int channels, const int* l
   s.y_stride_c = y_stride_c;
   s.y_stride_f = y_stride_f;
   s.max_frames = T;
+  s.max_len = max_len;
   const int rc = avz_launch_stft(p->cfg.n_fft, &s, stream);
   if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
   return rc;
@@ -407,6 +448,7 @@ extern "C" int avz_mask_features(const avz_plan* p, int layout, int batch, const
   s.x_stride = x_stride;
   s.ch_stride = ch_stride;
   s.max_frames = frames_for(max_len, p->cfg.hop);
+  s.max_len = max_len;
   s.feat = layout;
   s.F_out = feat;
   s.f_sb = s_b;
@@ -438,10 +480,11 @@ extern "C" int avz_srp_scan(const avz_plan* p, int batch, const int* len, int ma
   k.mic_d = c.mic_d;
   k.c_sound = c.c_sound;
   k.max_frames = frames_for(max_len, c.hop);
+  k.max_len = max_len;
   k.nchunk = p->nchunk;
-  k.part = p->part;
-  k.mwords = p->mwords;
-  k.peak_u = p->peak_u;
+  k.part = p->ws.part;
+  k.mwords = p->ws.mwords;
+  k.peak_u = p->ws.peak_u;
   avz::SrpArgs s{};
   s.n_angles = n_angles;
   s.angle_lo = angle_lo;

@@ -47,7 +47,8 @@ struct CGeo {
   static constexpr int MISC_OFF = TW_OFF + C::TW_BYTES;
   static constexpr int LDS_BYTES = MISC_OFF + 64;
   static_assert(BPT >= 1 && BPT * NT == N / 2, "bin mapping");
-  static_assert(2 * LDS_BYTES <= 160 * 1024, "two blocks per CU");
+  static constexpr int BLOCKS = C::BLOCKS_PER_CU;  // resident blocks per CU (= waves per SIMD)
+  static_assert(BLOCKS * LDS_BYTES <= 160 * 1024, "resident blocks per CU");
 };
 
 // Per-lane analysis window * 1/sum(win) and synthesis window * sum(win)/N terms.
@@ -94,10 +95,14 @@ __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<
                                            const typename KCfg<N>::Fft& fft, cf* spec,
                                            const cf* twid, const LaneMap<N>& lm) {
   using C = KCfg<N>;
+  float a0 = wc.a0, ac = wc.ac, as = wc.as;
+  opaque(a0);
+  opaque(ac);
+  opaque(as);
   static_for<0, C::PPL>([&](auto r) {
     constexpr int j = (C::IN_STRIDE * 32 / N) * r;  // 2 pi (IN_STRIDE r)/N = 2 pi j/32
     constexpr float cr = W32::c[j % 32], sr = -W32::s[j % 32];
-    const float w = fmaf(wc.as, sr, fmaf(-wc.ac, cr, wc.a0));
+    const float w = fmaf(as, sr, fmaf(-ac, cr, a0));
     v[r] = c_scale(v[r], w);
   });
   fft.forward(v, spec, twid);
@@ -155,7 +160,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
-  const int L = A.len[b];
+  const int L = min(A.len[b], A.max_len);  // a device length never exceeds the rows
   if (L < N) return;  // host validates; finalize reports NaN for a bad device length
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
@@ -400,13 +405,13 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
 // i, i + gridDim.x, ... so the twiddle table is built once per block and the batch is
 // spread evenly over the resident blocks (no second, partly idle round of short blocks).
 template <int N, int MASK, bool IRM>
-__global__ void __launch_bounds__(kCThreads, 2) avz_analysis_kernel(ChainArgs A) {
+__global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysis_kernel(ChainArgs A) {
   using G = CGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
   KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
   const int n_items = gx * A.batch;
-  if constexpr (N == 1024) {
+  if constexpr (N == 1024 && !AVZ_X1) {
     __syncthreads();
     cf tw_reg[31];
     Fft1024x2 f;
@@ -432,7 +437,7 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
   if (idx >= (long long)A.batch * F) return;
   const int b = (int)(idx / F), k = (int)(idx % F);
-  const int L = A.len[b];
+  const int L = min(A.len[b], A.max_len);  // a device length never exceeds the rows
   if (L < N) return;
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
@@ -471,7 +476,7 @@ __global__ void __launch_bounds__(kSrpThreads) avz_srp_kernel(ChainArgs A, SrpAr
   __shared__ double R[F][4];
   __shared__ double red[kSrpThreads / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int L = A.len[b];
+  const int L = min(A.len[b], A.max_len);  // a device length never exceeds the rows
   double* out = S.power_db + (long long)b * S.n_angles;
   if (L < N) {
     for (int i = tid; i < S.n_angles; i += kSrpThreads) out[i] = __builtin_nan("");
@@ -540,7 +545,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
-  const int L = A.len[b];
+  const int L = min(A.len[b], A.max_len);  // a device length never exceeds the rows
   if (L < N) return;
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
@@ -647,7 +652,9 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     AVZ_STAMP(5);
 #endif
     window_fft<N>(v, wc, fft, my_spec, twid, lm);
-    if (more) issue_loads(step + 1);  // in flight through apply, inverse FFT and OLA
+    // x2: the next step's loads fly through apply, inverse FFT and OLA; x1 issues them
+    // after the inverse FFT (its registers are needed there at four waves per SIMD)
+    if (!AVZ_X1 && more) issue_loads(step + 1);
     lds_barrier();
     AVZ_STAMP(6);
 
@@ -733,7 +740,28 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     AVZ_STAMP(7);
 
     // ---- inverse FFT of the packed pairs -> windowed frame contributions in slot 2p+1
-    if constexpr (N == 1024) {
+    if constexpr (N == 1024 && AVZ_X1) {
+      // two pairs: waves 0-1 run one 64-lane 1024-point transform each (register twiddles;
+      // output register k of lane (l, h) is sample l + 512 h + 32 k)
+      if (wave < NPAIR) {
+        cf u[16];
+        cf* Zi = slot_ptr<N>(lds, 2 * wave);
+        static_for<0, 16>([&](auto r) { u[r] = c_conj(Zi[64 * r + lane]); });
+        fft.forward(u, Zi, twid);
+        float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * wave + 1));
+        const int n0 = (lane & 31) + 512 * (lane >> 5);
+        float ws = wi_s, wcs = wi_c;
+        opaque(ws);
+        opaque(wcs);
+        static_for<0, 16>([&](auto k) {
+          constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+          const float w = fmaf(ws, sk, fmaf(-wcs, ck, 0.25f));
+          const int n = n0 + 32 * k;
+          Cp[n] = u[k].x * w;       // frame 2p   (real part of the inverse)
+          Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
+        });
+      }
+    } else if constexpr (N == 1024) {
       // four pairs, four waves: one 64-lane 1024-point transform each (x1 layout:
       // output register k of lane (l, h) is sample l + 512 h + 32 k)
       cf u[16];
@@ -764,6 +792,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
       });
     }
+    if (AVZ_X1 && more) issue_loads(step + 1);
     lds_barrier();
     AVZ_STAMP(8);
 
@@ -814,7 +843,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
 
 // Persistent grid over (chunk, utterance) items, as avz_analysis_kernel.
 template <int N, int PF>
-__global__ void __launch_bounds__(kCThreads, 2) avz_synthesis_kernel(ChainArgs A) {
+__global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_synthesis_kernel(ChainArgs A) {
   using G = CGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
   KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
@@ -831,7 +860,7 @@ __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
   __shared__ float red[NWAVE];
   const int c = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int L = A.len[b];
+  const int L = min(A.len[b], A.max_len);  // a device length never exceeds the rows
   if (L < N) {
     if (c == 0 && tid == 0 && A.peak) A.peak[b] = __builtin_nanf("");
     return;
@@ -921,7 +950,7 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   if (nch > a->nchunk) return -2;
   const dim3 grid(nch, a->batch);
   const int n_items = nch * a->batch;
-  const dim3 pgrid((unsigned)std::min(n_items, 2 * resident_cus()));  // ~2 blocks per CU
+  const dim3 pgrid((unsigned)std::min(n_items, CGeo<N>::BLOCKS * resident_cus()));
   constexpr int F = N / 2 + 1;
   const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
   hipEvent_t const* ev = reinterpret_cast<hipEvent_t const*>(a->events);
@@ -933,7 +962,8 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   mark(1);
   hipLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, *a);
   mark(2);
-  hipLaunchKernelGGL(k2, pgrid, dim3(kCThreads), lds, st, *a);
+  const dim3 sgrid((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus()));
+  hipLaunchKernelGGL(k2, sgrid, dim3(kCThreads), lds, st, *a);
   mark(3);
   hipLaunchKernelGGL(k3, grid, dim3(kCThreads), 0, st, *a);
   mark(4);
@@ -966,7 +996,7 @@ static int launch_srp_t(const ChainArgs* a, const SrpArgs* s, hipStream_t st) {
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
   const int n_items = nch * a->batch;
-  hipLaunchKernelGGL(k1, dim3((unsigned)std::min(n_items, 2 * resident_cus())), dim3(kCThreads),
+  hipLaunchKernelGGL(k1, dim3((unsigned)std::min(n_items, CGeo<N>::BLOCKS * resident_cus())), dim3(kCThreads),
                      lds, st, *a);
   hipLaunchKernelGGL(avz_srp_kernel<N>, dim3(a->batch), dim3(kSrpThreads), 0, st, *a, *s);
   return hipGetLastError() == hipSuccess ? 0 : -3;

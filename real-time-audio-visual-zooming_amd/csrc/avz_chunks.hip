@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(kCopyThreads) avz_chunk_split_kernel(ChunkSpli
 __global__ void __launch_bounds__(kCopyThreads) avz_chunk_merge_kernel(ChunkMergeArgs A) {
   __shared__ float red[kCopyThreads / 64];
   const int b = blockIdx.y;
-  const int L = A.len[b];
+  const int L = min(A.len[b], A.max_len);
   const int nch = (L + A.hop - 1) / A.hop;
   const float* io = A.item_out + (long long)A.item_base[b] * A.item_out_stride;
   float* y = A.y + (long long)b * A.y_stride;
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(kCopyThreads) avz_chunk_merge_kernel(ChunkMerg
 // y[b][n] /= peak[b] + norm_eps (inference.py:236). grid as the merge kernel.
 __global__ void __launch_bounds__(kCopyThreads) avz_chunk_scale_kernel(ChunkMergeArgs A) {
   const int b = blockIdx.y;
-  const int L = A.len[b];
+  const int L = min(A.len[b], A.max_len);
   const float s = 1.0f / (A.peak[b] + A.norm_eps);
   float* y = A.y + (long long)b * A.y_stride;
   const int n0 = 4 * (blockIdx.x * kCopyThreads + threadIdx.x);

@@ -51,6 +51,11 @@ __device__ __forceinline__ float bload_nn(rsrc_t r, int elem) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, elem * 4, 0, 0));
 }
 
+// Hide a value's provenance from the optimiser: per-iteration recomputation of
+// lane-constant terms (window weights) then stays in the loop instead of being hoisted
+// out and held in (or spilled from) registers for the whole kernel.
+__device__ __forceinline__ void opaque(float& x) { asm volatile("" : "+v"(x)); }
+
 // LDS-only barrier: leaves global loads (the next frame's prefetch) in flight.
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -58,8 +63,35 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// AVZ_X1: the N = 1024 chain kernels run one 1024-point FFT per wave (Fft1024, 16 points
+// per lane, one 8.4 KB LDS slot per wave) instead of two per wave (Fft1024x2, 32 points
+// per lane, two slots): a quarter of the LDS and about half the VGPRs per wave, so four
+// 4-wave blocks fit a CU (four waves per SIMD instead of two).
+#ifndef AVZ_X1
+#define AVZ_X1 0
+#endif
+
 template <int N>
 struct KCfg;
+#if AVZ_X1
+template <>
+struct KCfg<1024> {
+  using Fft = Fft1024;
+  static constexpr int PPL = Fft::PPL;       // 16 complex points per lane
+  static constexpr int FPW = 1;              // one FFT per wave
+  static constexpr int GROUP_BYTES = 32 * 33 * 8;
+  static constexpr int WAVE_BYTES = GROUP_BYTES;
+  static constexpr int IN_STRIDE = 64;       // lane L, reg r <-> x[64 r + L]
+  static constexpr int OUT_STRIDE = 32;      // lane (k1, h), reg k <-> X[k1 + 32 k + 512 h]
+  static constexpr int TW_BYTES = Fft1024::TW_ENTRIES * 8;  // P, Q table (3 KB)
+  static constexpr int BLOCKS_PER_CU = 4;
+#ifdef AVZ_SYN_BLOCKS
+  static constexpr int SYN_BLOCKS_PER_CU = AVZ_SYN_BLOCKS;
+#else
+  static constexpr int SYN_BLOCKS_PER_CU = 4;
+#endif
+};
+#else
 template <>
 struct KCfg<1024> {
   using Fft = Fft1024x2;
@@ -70,7 +102,10 @@ struct KCfg<1024> {
   static constexpr int IN_STRIDE = 32;       // sample stride between registers
   static constexpr int OUT_STRIDE = 32;      // bin/time stride between registers
   static constexpr int TW_BYTES = 32 * 32 * 8;  // block-shared W1024^{l k1} table
+  static constexpr int BLOCKS_PER_CU = 2;
+  static constexpr int SYN_BLOCKS_PER_CU = 2;
 };
+#endif
 template <>
 struct KCfg<512> {
   using Fft = Fft512x2;
@@ -81,6 +116,8 @@ struct KCfg<512> {
   static constexpr int IN_STRIDE = 32;
   static constexpr int OUT_STRIDE = 16;
   static constexpr int TW_BYTES = 0;
+  static constexpr int BLOCKS_PER_CU = 2;
+  static constexpr int SYN_BLOCKS_PER_CU = 2;
 };
 
 template <int N, int NT>
@@ -115,7 +152,11 @@ struct LaneMap {
   int grp;    // lane group (N=512: which of the two FFTs; N=1024: 0)
   int out0;   // output index of register 0
   __device__ __forceinline__ void init(int lane) {
-    if constexpr (N == 1024) {
+    if constexpr (N == 1024 && AVZ_X1) {
+      in0 = lane;
+      grp = 0;
+      out0 = (lane & 31) + 512 * (lane >> 5);
+    } else if constexpr (N == 1024) {
       in0 = lane & 31;
       grp = lane >> 5;
       out0 = lane & 31;

@@ -222,6 +222,43 @@ struct Fft1024 {
     xhalf_dit<32>(v, sgn);
   }
 
+  // Interface shared with Fft1024x2 / Fft512x2 (the chain kernels call these): P and Q
+  // come from a 3 KB block table pq[j][l] (j < 4: W^{l j}; 4 + 4 h + i: W^{l (4 i + 16 h)})
+  // read per transform, so they hold no registers across the kernel's other phases.
+  static constexpr int TW_ENTRIES = 12 * 32;
+  __device__ static void fill_twiddles(cf* tab, int tid, int nthreads) {
+    for (int e = tid; e < TW_ENTRIES; e += nthreads) {
+      const int j = e >> 5, ll = e & 31;
+      const int m = j < 4 ? j : 4 * ((j - 4) & 3) + 16 * ((j - 4) >> 2);
+      tab[e] = unit_root((double)(ll * m) / N);
+    }
+  }
+  __device__ __forceinline__ void forward(cf (&v)[16], cf* scratch, const cf* tab) const {
+    cf p[4], q[4];
+    static_for<0, 4>([&](auto j) {
+      p[j] = tab[j * 32 + l];
+      q[j] = tab[(4 + 4 * h + j) * 32 + l];
+    });
+    dft16(v);
+    xhalf_dit<32>(v, sgn);
+    static_for<0, 16>([&](auto k) {
+      const cf tw = ((k & 3) == 0) ? q[k >> 2] : c_mul(p[k & 3], q[k >> 2]);
+      v[k] = c_mul(v[k], tw);
+    });
+    static_for<0, 16>([&](auto k) { scratch[(k + 16 * h) * 33 + l] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = scratch[l * 33 + 2 * r + h]; });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<32>(v, sgn);
+  }
+  // lane geometry only (the table form needs no P, Q registers)
+  __device__ __forceinline__ void init_lane(int lane) {
+    l = lane & 31;
+    h = lane >> 5;
+    sgn = h ? -1.0f : 1.0f;
+  }
+
   // The same transform for a lane that did not init(): twiddles W1024^{l k1} come
   // from a block-shared LDS table tw[k1 * 32 + l] (Fft1024x2::fill_twiddles).
   __device__ __forceinline__ static void forward_tw(cf (&v)[16], cf* scratch, const cf* tw,

@@ -13,7 +13,8 @@ enum : int { BF_MVDR = 0, BF_HYBRID_NULL = 1 };
 // Everything the analysis / solve / synthesis / finalize chain needs, passed by value.
 struct ChainArgs {
   int batch;
-  const int* len;             // [B] samples per utterance (device)
+  const int* len;             // [B] samples per utterance (device; kernels clamp to max_len)
+  int max_len;                // host-validated upper bound of len[] (the buffers' extent)
   const float* mix;           // [B][2][..] planar
   long long mix_stride;       // floats between utterances
   long long ch_stride;        // floats between the two mic channels
@@ -51,7 +52,8 @@ struct ChainArgs {
 
 struct StftArgs {
   int batch, channels;        // channels 1 or 2
-  const int* len;
+  const int* len;             // clamped to max_len in the kernel
+  int max_len;
   const float* x;             // [B][C][..]
   long long x_stride, ch_stride;
   float* Y;                   // complex64 [B][C][F][t_stride] as float2

@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(kStftThreads, 1) avz_stft_kernel(StftArgs A) {
   const int b = blockIdx.x;
   const int f0 = blockIdx.y * NSLOT;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int L = A.len[b];
+  const int L = min(A.len[b], A.max_len);
   const int T = (L + H - 1) / H + 1;
   if (f0 >= T || L < N) return;
   __syncthreads();

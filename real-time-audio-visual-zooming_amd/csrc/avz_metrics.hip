@@ -33,7 +33,7 @@ template <bool VEC>
 __global__ void __launch_bounds__(kMetThreads) avz_metrics_sums_kernel(MetricsArgs A) {
   __shared__ double red[kMetThreads / 64][6];
   const int b = blockIdx.y;
-  const int L = A.len[b];
+  const int L = min(A.len[b], A.max_len);
   const float* o = A.est + (long long)b * A.est_stride;
   const float* t = A.tgt + (long long)b * A.tgt_stride;
   const float* i = A.itf + (long long)b * A.itf_stride;
