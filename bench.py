@@ -362,9 +362,12 @@ def main():
 
     t_max = float(elapsed.item())
     value = world * info["bins"] * K / t_max
-    # Algorithmic bytes: the analysis kernel reads the mic (+ reference)
-    # streams, 4 B per sample each (ibm: 15.97 B per TF-bin); the whole chain adds the
-    # output stream (ibm: 19.96 B per TF-bin).
+    # Roofline, SURVEY 8(d): achieved = TF-bins/s x bytes_per_bin with bytes_per_bin =
+    # (fp32 streams) x 4 H / F: every 4-byte sample stream costs 4 H / F B per TF-bin
+    # (3.992 at 1024/512). ibm: 2 mic + 2 references + output = 19.96 B/bin; ipd: 2 mic +
+    # output = 11.98; external mask: + 4 B/bin of mask = 15.98. Per GPU (peak is per GPU).
+    per_stream = 4.0 * HOP / (N_FFT // 2 + 1)
+    bpb = {"ibm": 5 * per_stream, "ipd": 3 * per_stream, "unet": 3 * per_stream + 4.0}[args.workload]
     alg_analysis, alg_chain = info["alg_analysis"], info["alg_chain"]
     traffic = {}
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -374,31 +377,35 @@ def main():
             traffic = pm.get("hbm_bytes_per_launch", {})
             if not isinstance(traffic, dict):
                 traffic = {}
+    achieved = value / world * bpb / 1e9
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("chain"),
+            "bytes_per_bin": bpb,
+            "formula": "SURVEY 8(d): value / n_gpus x bytes_per_bin / 8e12",
+            "kernel": "avz_mvdr_batch chain (analysis + solve + synthesis + finalize)",
+            "kernel_ms": chain_ms, "alg_bytes_per_launch": info["bins"] * bpb}
     if kt:
         dom_ms = kt["analysis_timed"]  # HIP events on the launch stream, over the timed steps
-        roof = {"bound": "hbm", "achieved": alg_analysis / (dom_ms * 1e-3) / 1e9,
-                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": alg_analysis / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "traffic": traffic.get("analysis"),
-                "kernel": info["kernel"], "kernel_ms": dom_ms,
-                "alg_bytes_per_launch": alg_analysis,
-                "kernels_ms": {k: kt[k] for k in plan.KERNELS},  # separate untimed pass
-                "kernels_ms_note": "kernel_ms: analysis over the timed steps (two events "
-                                   "per step); kernels_ms/chain: all four kernels in an "
-                                   "untimed pass after them",
-                "chain": {"achieved": alg_chain / (chain_ms * 1e-3) / 1e9, "ms": chain_ms,
-                          "alg_bytes_per_launch": alg_chain,
-                          "frac": alg_chain / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                          "traffic": traffic.get("chain")}}
-    else:
-        roof = {"bound": "hbm", "achieved": alg_chain / (step_ms * 1e-3) / 1e9,
-                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": alg_chain / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "traffic": traffic.get("chain"), "kernel": "avz_mvdr_batch chain",
-                "kernel_ms": step_ms, "alg_bytes_per_launch": alg_chain}
+        roof["kernels_ms"] = {k: kt[k] for k in plan.KERNELS}  # separate untimed pass
+        roof["kernels_ms_note"] = ("kernel_ms: the four kernels in an untimed pass after the "
+                                   "timed steps; dominant_kernel.kernel_ms: analysis over the "
+                                   "timed steps (two events per step)")
+        roof["dominant_kernel"] = {
+            "kernel": info["kernel"], "kernel_ms": dom_ms,
+            "alg_bytes_per_launch": alg_analysis,
+            "achieved": alg_analysis / (dom_ms * 1e-3) / 1e9,
+            "frac": alg_analysis / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "traffic": traffic.get("analysis")}
+        roof["chain_events"] = {"ms": chain_ms, "alg_bytes_per_launch": alg_chain,
+                                "achieved": alg_chain / (chain_ms * 1e-3) / 1e9,
+                                "frac": alg_chain / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     if rank == 0:
-        cfg = {"workload": WORKLOAD_TEXT[args.workload].format(
-            B=B, k=args.interferers, unet_dtype=args.unet_dtype, n=N_FFT, h=HOP),
+        wtext = WORKLOAD_TEXT[args.workload].format(
+            B=B, k=args.interferers, unet_dtype=args.unet_dtype, n=N_FFT, h=HOP)
+        if args.workload == "ibm" and args.interferers == 3 and B == 512:
+            wtext = ("configs[2] per-GPU shard (B=4096 over 8 GPUs = 512 utterances/GPU): "
+                     + wtext.split(": ", 1)[1])
+        cfg = {"workload": wtext,
                "batch_per_gpu": B, "global_batch": B * world, "samples": S,
                "n_fft": N_FFT, "hop": HOP, "parallelism":
                f"utterance-sharded x{world}, RCCL metric all-reduce only"}

@@ -58,6 +58,10 @@ extern "C" {
 /* weights of a bin whose loaded covariance is singular (A8) */
 #define AVZ_FALLBACK_MIC0 0 /* w = [1, 0], oracle_debug.py:78-79, masked_mvdr.py:120-122  */
 #define AVZ_FALLBACK_MEAN 1 /* w = ones/2, oracle_reverb.py:133-135                       */
+#define AVZ_FALLBACK_BATCH 2 /* batch_mvdr (tf_lite_version/inference.py:143-157): one
+                               np.linalg.solve over all bins of a call, so a singular bin sends
+                               EVERY bin of that item to w~ = [1, 0]^T, which is then
+                               normalised like the others: w = [1/(conj(d0) + 1e-10), 0]     */
 
 /* beamformers (A8 / A14) */
 #define AVZ_BF_MVDR 0       /* (R/(sum m + 1e-6) + sigma I)^-1 d, normalised; oracle_debug.py:66-79 */
@@ -137,6 +141,71 @@ int avz_mvdr_batch(const avz_plan* plan, const avz_batch_args* args, void* hip_s
 /* Device bytes of a per-call workspace for `batch` utterances of at most max_len samples
  * (negative AVZ_ERR_* on bad arguments). */
 long long avz_mvdr_workspace_bytes(const avz_plan* plan, int batch, int max_len);
+
+/* ------------------------------------------------------------------ stage exports
+ * The chain of avz_mvdr_batch, one stage at a time (stage-wise parity with
+ * rt_av_zoom/core/oracle_debug.py:42-64 / :66-79 / :80-94):
+ *  avz_mvdr_covariance  STFT -> mask -> masked covariance sums, args->cov_out[b][F][5]
+ *                       (sum m|y0|^2, sum m|y1|^2, Re/Im sum m y0 y1*, sum m; fp64);
+ *                       args->out unused. Inputs as avz_mvdr_batch for the plan's mask mode.
+ *  avz_solve_covariance cov[b][F][5] -> weights w[b][F][4] (Re w0, Im w0, Re w1, Im w1;
+ *                       16-byte aligned) with the plan's beamformer, sigma, fmin and
+ *                       fallback; steer = optional [F][2] complex128 steering vectors
+ *                       (NULL: the plan's); fallback = optional [batch] flags (NULL: the
+ *                       plan's own buffer, calls then serialised).
+ *  avz_apply_istft      STFT of args->mix -> S = w^H y (x args->ext_mask as a gain when
+ *                       non-NULL, mask_bins / mask_frames as for EXTERNAL) -> iSTFT/OLA ->
+ *                       args->out (peak-normalised per the plan), args->peak.
+ * Device arrays; the same workspace rules as avz_mvdr_batch. */
+int avz_mvdr_covariance(const avz_plan* plan, const avz_batch_args* args, void* hip_stream);
+int avz_solve_covariance(const avz_plan* plan, int batch, const double* cov, float* w,
+                         const double* steer, int* fallback, void* hip_stream);
+int avz_apply_istft(const avz_plan* plan, const avz_batch_args* args, const float* w,
+                    void* hip_stream);
+
+/* ------------------------------------------------------------------ spectral domain
+ * For callers that already hold an STFT. avz_beamform_spectral replaces, per item b,
+ *  - beamformer AVZ_BF_MVDR: batch_mvdr(Y, mask, f_bins, d_vectors, sigma)
+ *    (rt_av_zoom/core/tf_lite_version/inference.py:85-179; plan: weight_eps 1e-10,
+ *    fmin_hz 0, singular_fallback AVZ_FALLBACK_BATCH, sigma = SIGMA);
+ *  - beamformer AVZ_BF_HYBRID_NULL: hybrid_hard_null_bf(Y, mask, f_bins)
+ *    (Final_pipeline/src/inference.py:28-98; plan: weight_eps 0, bypass_hz 200,
+ *    cond_max 10),
+ * with the plan's post-filter fused (AVZ_PF_EXT_FLOOR: x max(M, pf_floor), the TFLite
+ * driver's S_out * np.maximum(mask, 0.05), inference.py:350; AVZ_PF_EXT_MUL: x M,
+ * Final_pipeline/src/inference.py:219; AVZ_PF_NONE: the bare operator). The plan's mask
+ * mode must be AVZ_MASK_EXTERNAL (mask = target probability, noise weight 1 - M).
+ * Y: complex64 [b][m][k][t] (interleaved re/im; m = mic 0, 1; t contiguous), strides in
+ * complex elements; mask [b][k][t] float; S: complex64 [b][k][t]. steer: optional [F][2]
+ * complex128 (batch_mvdr's d_vectors; NULL: the plan's table). cov_out / w_out: optional
+ * per-bin covariance sums / weights; fallback: optional [batch] int flags (1 where an
+ * item took the item-level fallback; NULL: the plan's own buffer). */
+typedef struct avz_spectral_args {
+  int batch;               /* items (one reference call each)                              */
+  int frames;              /* T frames per item                                            */
+  const float* Y;
+  long long y_stride_b, y_stride_m, y_stride_f;
+  const float* mask;
+  long long mask_stride_b, mask_stride_f;
+  const double* steer;
+  float* S;
+  long long s_stride_b, s_stride_f;
+  double* cov_out;
+  float* w_out;
+  int* fallback;
+} avz_spectral_args;
+int avz_beamform_spectral(const avz_plan* plan, const avz_spectral_args* args, void* hip_stream);
+
+/* scipy.signal.istft(S, fs, nperseg=n_fft, noverlap=n_fft/2) of complex64 S[b][k][t]
+ * (t contiguous; strides in complex elements) for `frames` frames per item: out[b] gets
+ * (frames - 1) * hop samples (<= max_samples), peak-normalised per the plan; peak[b] =
+ * max|out| before normalisation (or NULL). The same workspace rules as avz_mvdr_batch
+ * (workspace bytes: avz_mvdr_workspace_bytes(plan, batch, (frames - 1) * hop)). Replaces
+ * the istft calls at oracle_debug.py:93, tf_lite_version/inference.py:352,
+ * Final_pipeline/src/inference.py:222. */
+int avz_istft(const avz_plan* plan, int batch, int frames, const float* S, long long s_stride_b,
+              long long s_stride_f, float* out, long long out_stride, float* peak,
+              void* workspace, long long workspace_bytes, void* hip_stream);
 
 /* Diagnostics: record HIP events around the kernels of every avz_mvdr_batch call on
  * this plan: enable 1 = all four (analysis, solve, synthesis, finalize), 2 = the analysis

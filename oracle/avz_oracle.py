@@ -213,6 +213,49 @@ def mvdr_weights_vec(R: np.ndarray, f: np.ndarray, sigma: float, angle: float, d
     return W
 
 
+def get_all_steering_vectors(f_bins: np.ndarray, angle_deg: float, d: float,
+                             c: float) -> np.ndarray:
+    """rt_av_zoom/core/tf_lite_version/inference.py:53-81: [F, 2, 1] complex128 far-field
+    vectors exp(-1j 2 pi f tau_m), tau_1 = (d/2) cos(theta)/c, tau_2 = (d/2) cos(theta - pi)/c."""
+    th = np.deg2rad(angle_deg)
+    om = 2 * np.pi * np.asarray(f_bins)
+    sv = np.stack([np.exp(-1j * om * ((d / 2) * np.cos(th) / c)),
+                   np.exp(-1j * om * ((d / 2) * np.cos(th - np.pi) / c))], axis=0)
+    return sv.T[:, :, None]
+
+
+def batch_mvdr(Y: np.ndarray, mask: np.ndarray, f_bins, d_vectors: np.ndarray,
+               sigma: float) -> np.ndarray:
+    """rt_av_zoom/core/tf_lite_version/inference.py:85-179 restated with its dtypes: the
+    noise weight 1 - mask (float32 for a float32 mask), Y * sqrt(w + 1e-10) and the
+    covariance in complex64 (:103-117), / (sum w + 1e-6) (:121), + sigma I promotes to
+    complex128 (:127-131), ONE batched solve whose LinAlgError sends every bin to
+    w~ = [1, 0] (:139-153), w = w~ / (d^H w~ + 1e-10) (:159-163), S = w^H y (:169-175).
+    f_bins is unused, as in the reference. Returns S [F, T] complex128."""
+    Yp = np.transpose(Y, (1, 0, 2))
+    mn = (1.0 - mask)[:, None, :]
+    Yw = Yp * np.sqrt(mn + 1e-10)
+    R = np.einsum('fmt,fnt->fmn', Yw, Yw.conj())
+    R = R / (np.sum(mn, axis=2)[:, :, None] + 1e-6)
+    R = R + sigma * np.eye(2)[None]
+    try:
+        wu = np.linalg.solve(R, d_vectors)
+    except np.linalg.LinAlgError:
+        wu = np.zeros_like(d_vectors)
+        wu[:, 0, :] = 1.0
+    den = np.matmul(np.transpose(d_vectors.conj(), (0, 2, 1)), wu) + 1e-10
+    w = wu / den
+    return np.matmul(np.transpose(w.conj(), (0, 2, 1)), Yp)[:, 0, :]
+
+
+def hybrid_hard_null_bf(Y: np.ndarray, mask: np.ndarray, f_bins: np.ndarray,
+                        d: float = 0.08) -> np.ndarray:
+    """Final_pipeline/src/inference.py:28-98 as an operator: S[F, T] = w^H y with the
+    loop-faithful per-bin weights (hybrid_weights_loop; bypass bins pass Y[0])."""
+    W = hybrid_weights_loop(Y, mask, f_bins, d=d)
+    return apply_weights(W, Y)
+
+
 def apply_weights(W: np.ndarray, Y: np.ndarray) -> np.ndarray:
     """S[f,t] = w^H Y[:, f, t] (oracle_debug.py:80)."""
     return np.conj(W[:, 0])[:, None] * Y[0] + np.conj(W[:, 1])[:, None] * Y[1]

@@ -26,7 +26,7 @@ AVZ_ERR_ALIGN = -5
 
 MASK_IBM, MASK_IPD, MASK_EXTERNAL, MASK_ONES = 0, 1, 2, 3
 PF_NONE, PF_IBM_TARGET, PF_EXT_FLOOR, PF_EXT_MUL, PF_IRM = 0, 1, 2, 3, 4
-FALLBACK_MIC0, FALLBACK_MEAN = 0, 1
+FALLBACK_MIC0, FALLBACK_MEAN, FALLBACK_BATCH = 0, 1, 2
 NORM_NONE, NORM_PEAK = 0, 1
 BF_MVDR, BF_HYBRID_NULL = 0, 1
 FEAT_LOGMAG_IPD, FEAT_TFLITE = 1, 2
@@ -37,6 +37,8 @@ EXPORTED = [
     "avz_chunk_split", "avz_chunk_merge", "avz_mask_features", "avz_srp_scan",
     "avz_projection_metrics", "avz_scene_workspace_bytes", "avz_scene_mix", "avz_strerror",
     "avz_last_hip_error", "avz_version", "avz_mvdr_workspace_bytes",
+    "avz_mvdr_covariance", "avz_solve_covariance", "avz_apply_istft", "avz_beamform_spectral",
+    "avz_istft",
 ]
 
 
@@ -65,6 +67,18 @@ class AvzBatchArgs(ct.Structure):
         ("cov_out", ct.c_void_p), ("w_out", ct.c_void_p),
         ("mask_bins", ct.c_int), ("mask_frames", ct.c_int),
         ("workspace", ct.c_void_p), ("workspace_bytes", ct.c_longlong),
+    ]
+
+
+class AvzSpectralArgs(ct.Structure):
+    _fields_ = [
+        ("batch", ct.c_int), ("frames", ct.c_int),
+        ("Y", ct.c_void_p), ("y_stride_b", ct.c_longlong), ("y_stride_m", ct.c_longlong),
+        ("y_stride_f", ct.c_longlong),
+        ("mask", ct.c_void_p), ("mask_stride_b", ct.c_longlong), ("mask_stride_f", ct.c_longlong),
+        ("steer", ct.c_void_p),
+        ("S", ct.c_void_p), ("s_stride_b", ct.c_longlong), ("s_stride_f", ct.c_longlong),
+        ("cov_out", ct.c_void_p), ("w_out", ct.c_void_p), ("fallback", ct.c_void_p),
     ]
 
 
@@ -101,6 +115,15 @@ def _load():
     lib.avz_mvdr_batch.argtypes = [P, ct.POINTER(AvzBatchArgs), P]
     lib.avz_mvdr_workspace_bytes.argtypes = [P, ct.c_int, ct.c_int]
     lib.avz_mvdr_workspace_bytes.restype = ct.c_longlong
+    lib.avz_mvdr_covariance.argtypes = [P, ct.POINTER(AvzBatchArgs), P]
+    lib.avz_solve_covariance.argtypes = [P, ct.c_int, P, P, P, P, P]
+    lib.avz_apply_istft.argtypes = [P, ct.POINTER(AvzBatchArgs), P, P]
+    lib.avz_beamform_spectral.argtypes = [P, ct.POINTER(AvzSpectralArgs), P]
+    lib.avz_istft.argtypes = [P, ct.c_int, ct.c_int, P, ct.c_longlong, ct.c_longlong, P,
+                              ct.c_longlong, P, P, ct.c_longlong, P]
+    for name in ("avz_mvdr_covariance", "avz_solve_covariance", "avz_apply_istft",
+                 "avz_beamform_spectral", "avz_istft"):
+        getattr(lib, name).restype = ct.c_int
     lib.avz_stft.argtypes = [P, ct.c_int, ct.c_int, P, ct.c_int, P, ct.c_longlong, ct.c_longlong,
                              P, ct.c_longlong, ct.c_longlong, ct.c_longlong, P]
     I, LL = ct.c_int, ct.c_longlong

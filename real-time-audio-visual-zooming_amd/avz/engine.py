@@ -20,7 +20,8 @@ MASKS = {"ibm": _lib.MASK_IBM, "ipd": _lib.MASK_IPD, "external": _lib.MASK_EXTER
          "ones": _lib.MASK_ONES}
 POSTFILTERS = {"none": _lib.PF_NONE, "ibm": _lib.PF_IBM_TARGET, "floor": _lib.PF_EXT_FLOOR,
                "mul": _lib.PF_EXT_MUL, "irm": _lib.PF_IRM}
-FALLBACKS = {"mic0": _lib.FALLBACK_MIC0, "mean": _lib.FALLBACK_MEAN}
+FALLBACKS = {"mic0": _lib.FALLBACK_MIC0, "mean": _lib.FALLBACK_MEAN,
+             "batch": _lib.FALLBACK_BATCH}
 NORMS = {"none": _lib.NORM_NONE, "peak": _lib.NORM_PEAK}
 BEAMFORMERS = {"mvdr": _lib.BF_MVDR, "hybrid_null": _lib.BF_HYBRID_NULL}
 
@@ -142,14 +143,9 @@ class MVDRPlan:
         n = self.workspace_bytes(batch, max_len)
         return torch.empty((max(n, 1) + 255) // 256 * 256, dtype=torch.uint8, device=device)
 
-    def run(self, mix: torch.Tensor, lengths: torch.Tensor | None = None, *,
-            max_len: int | None = None, ref_tgt=None, ref_int=None, ext_mask=None,
-            out: torch.Tensor | None = None, peak: torch.Tensor | None = None,
-            cov_out=None, w_out=None, workspace: torch.Tensor | None = None, stream=None):
-        """mix: [B, 2, S] float32 (device); lengths: [B] int32 (device, default S).
-        ref_tgt/ref_int: [B, S] (IBM); ext_mask: [B, F, T] target probability (EXTERNAL).
-        workspace: optional uint8 device tensor of >= workspace_bytes(B, max_len) bytes.
-        Returns (out [B, >= out_len], peak [B])."""
+    def _batch_args(self, mix, lengths, max_len, ref_tgt, ref_int, ext_mask, out, peak,
+                    cov_out, w_out, workspace, need_out=True):
+        """Validated avz_batch_args of a time-domain call (shared by run and the stages)."""
         if not mix.is_cuda:
             raise ValueError("mix must be a device tensor")
         if mix.dtype != torch.float32 or mix.dim() != 3 or mix.shape[1] != 2:
@@ -169,16 +165,20 @@ class MVDRPlan:
         if max_len > S:
             raise ValueError(f"max_len {max_len} exceeds the {S} samples of mix")
         T = self.frames(max_len)
-        if out is None:
-            out = self.alloc_out(B, max_len, dev)
-        if peak is None:
-            peak = torch.empty((B,), dtype=torch.float32, device=dev)
-        if out.dtype != torch.float32 or out.dim() != 2 or out.shape[0] < B or \
-                out.shape[1] < self.out_len(max_len) or out.stride(1) != 1:
-            raise ValueError("out must be float32 [>= B, >= out_len(max_len)]")
-        if peak.dtype != torch.float32 or peak.numel() < B or not peak.is_contiguous():
-            raise ValueError("peak must be a contiguous float32 tensor of >= B entries")
         a = AvzBatchArgs()
+        if need_out:
+            if out is None:
+                out = self.alloc_out(B, max_len, dev)
+            if peak is None:
+                peak = torch.empty((B,), dtype=torch.float32, device=dev)
+            if out.dtype != torch.float32 or out.dim() != 2 or out.shape[0] < B or \
+                    out.shape[1] < self.out_len(max_len) or out.stride(1) != 1:
+                raise ValueError("out must be float32 [>= B, >= out_len(max_len)]")
+            if peak.dtype != torch.float32 or peak.numel() < B or not peak.is_contiguous():
+                raise ValueError("peak must be a contiguous float32 tensor of >= B entries")
+            a.out = out.data_ptr()
+            a.out_stride = out.stride(0)
+            a.peak = peak.data_ptr()
         a.batch = B
         a.len = lengths.data_ptr()
         a.max_len = int(max_len)
@@ -205,9 +205,11 @@ class MVDRPlan:
             a.ext_mask = ext_mask.data_ptr()
             a.mask_stride_b, a.mask_stride_f, a.mask_stride_t = ext_mask.stride()
             a.mask_bins, a.mask_frames = ext_mask.shape[1], ext_mask.shape[2]
-        a.out = out.data_ptr()
-        a.out_stride = out.stride(0)
-        a.peak = peak.data_ptr()
+        for name, t, last in (("cov_out", cov_out, 5), ("w_out", w_out, 4)):
+            if t is not None and (not t.is_cuda or not t.is_contiguous() or t.numel() < B * self.F * last
+                                  or t.dtype != (torch.float64 if last == 5 else torch.float32)):
+                raise ValueError(f"{name} must be a contiguous device tensor of "
+                                 f"[B, F, {last}] {'float64' if last == 5 else 'float32'}")
         a.cov_out = 0 if cov_out is None else cov_out.data_ptr()
         a.w_out = 0 if w_out is None else w_out.data_ptr()
         if workspace is not None:
@@ -215,7 +217,142 @@ class MVDRPlan:
                 raise ValueError("workspace must be a uint8 device tensor")
             a.workspace = workspace.data_ptr()
             a.workspace_bytes = workspace.numel()
+        return a, out, peak
+
+    def run(self, mix: torch.Tensor, lengths: torch.Tensor | None = None, *,
+            max_len: int | None = None, ref_tgt=None, ref_int=None, ext_mask=None,
+            out: torch.Tensor | None = None, peak: torch.Tensor | None = None,
+            cov_out=None, w_out=None, workspace: torch.Tensor | None = None, stream=None):
+        """mix: [B, 2, S] float32 (device); lengths: [B] int32 (device, default S).
+        ref_tgt/ref_int: [B, S] (IBM); ext_mask: [B, F, T] target probability (EXTERNAL).
+        workspace: optional uint8 device tensor of >= workspace_bytes(B, max_len) bytes.
+        Returns (out [B, >= out_len], peak [B])."""
+        a, out, peak = self._batch_args(mix, lengths, max_len, ref_tgt, ref_int, ext_mask, out,
+                                        peak, cov_out, w_out, workspace)
         check(lib.avz_mvdr_batch(self._h, ct.byref(a), _stream_handle(stream)), "avz_mvdr_batch")
+        return out, peak
+
+    # ------------------------------------------------------------------ stage exports
+    def covariance(self, mix, lengths=None, *, max_len=None, ref_tgt=None, ref_int=None,
+                   ext_mask=None, cov_out=None, workspace=None, stream=None) -> torch.Tensor:
+        """STFT -> mask -> masked covariance sums (avz_mvdr_covariance): [B, F, 5] float64
+        (sum m|y0|^2, sum m|y1|^2, Re/Im sum m y0 conj(y1), sum m); oracle_debug.py:42-64."""
+        B = mix.shape[0]
+        if cov_out is None:
+            cov_out = torch.empty((B, self.F, 5), dtype=torch.float64, device=mix.device)
+        a, _, _ = self._batch_args(mix, lengths, max_len, ref_tgt, ref_int, ext_mask, None, None,
+                                   cov_out, None, workspace, need_out=False)
+        check(lib.avz_mvdr_covariance(self._h, ct.byref(a), _stream_handle(stream)),
+              "avz_mvdr_covariance")
+        return cov_out
+
+    def solve_covariance(self, cov: torch.Tensor, *, steer=None, w=None, fallback=None,
+                         stream=None) -> torch.Tensor:
+        """Covariance sums [B, F, 5] float64 -> weights [B, F, 4] float32 (Re w0, Im w0,
+        Re w1, Im w1) with the plan's beamformer (avz_solve_covariance; oracle_debug.py:66-79).
+        steer: optional [F, 2] complex128 device tensor; fallback: optional [B] int32."""
+        if cov.dtype != torch.float64 or cov.dim() != 3 or cov.shape[1:] != (self.F, 5) \
+                or not cov.is_contiguous() or not cov.is_cuda:
+            raise ValueError("cov must be a contiguous float64 [B, F, 5] device tensor")
+        B = cov.shape[0]
+        if w is None:
+            w = torch.empty((B, self.F, 4), dtype=torch.float32, device=cov.device)
+        st = self._steer_ptr(steer)
+        fb = self._fallback_ptr(fallback, B)
+        check(lib.avz_solve_covariance(self._h, B, ct.c_void_p(cov.data_ptr()),
+                                       ct.c_void_p(w.data_ptr()), st, fb, _stream_handle(stream)),
+              "avz_solve_covariance")
+        return w
+
+    def apply_istft(self, mix, w: torch.Tensor, lengths=None, *, max_len=None, gain=None,
+                    out=None, peak=None, workspace=None, stream=None):
+        """STFT of mix -> S = w^H y (x gain [B, F, T] when given) -> iSTFT/OLA
+        (avz_apply_istft; oracle_debug.py:80-94). Returns (out, peak)."""
+        if w.dtype != torch.float32 or not w.is_contiguous() or not w.is_cuda \
+                or w.numel() < mix.shape[0] * self.F * 4:
+            raise ValueError("w must be a contiguous float32 [B, F, 4] device tensor")
+        a, out, peak = self._batch_args(mix, lengths, max_len, None, None, gain, out, peak, None,
+                                        None, workspace)
+        check(lib.avz_apply_istft(self._h, ct.byref(a), ct.c_void_p(w.data_ptr()),
+                                  _stream_handle(stream)), "avz_apply_istft")
+        return out, peak
+
+    # ------------------------------------------------------------------ spectral domain
+    def _steer_ptr(self, steer):
+        if steer is None:
+            return None
+        if steer.dtype != torch.complex128 or steer.shape != (self.F, 2) or not steer.is_cuda \
+                or not steer.is_contiguous():
+            raise ValueError("steer must be a contiguous complex128 [F, 2] device tensor")
+        return ct.c_void_p(steer.data_ptr())
+
+    def _fallback_ptr(self, fallback, B):
+        if fallback is None:
+            return None
+        if fallback.dtype != torch.int32 or fallback.numel() < B or not fallback.is_cuda:
+            raise ValueError("fallback must be an int32 device tensor of >= B entries")
+        return ct.c_void_p(fallback.data_ptr())
+
+    def beamform_spectral(self, Y: torch.Tensor, mask: torch.Tensor, *, steer=None, S=None,
+                          cov_out=None, w_out=None, fallback=None, stream=None) -> torch.Tensor:
+        """Y [B, 2, F, T] complex64, mask [B, F, T] float32 target probability -> S [B, F, T]
+        complex64 (avz_beamform_spectral: batch_mvdr or hybrid_hard_null_bf per the plan's
+        beamformer, the plan's post-filter fused)."""
+        if Y.dtype != torch.complex64 or Y.dim() != 4 or Y.shape[1] != 2 or Y.shape[2] != self.F \
+                or Y.stride(3) != 1 or not Y.is_cuda:
+            raise ValueError(f"Y must be complex64 [B, 2, {self.F}, T] (t contiguous) on the device")
+        B, _, _, T = Y.shape
+        if mask.dtype != torch.float32 or mask.dim() != 3 or tuple(mask.shape) != (B, self.F, T) \
+                or mask.stride(2) != 1 or not mask.is_cuda:
+            raise ValueError(f"mask must be float32 [{B}, {self.F}, {T}] (t contiguous)")
+        if S is None:
+            S = torch.empty((B, self.F, T), dtype=torch.complex64, device=Y.device)
+        if S.dtype != torch.complex64 or tuple(S.shape) != (B, self.F, T) or S.stride(2) != 1:
+            raise ValueError("S must be complex64 [B, F, T] (t contiguous)")
+        for name, t, last, dt in (("cov_out", cov_out, 5, torch.float64),
+                                  ("w_out", w_out, 4, torch.float32)):
+            if t is not None and (t.dtype != dt or not t.is_contiguous() or not t.is_cuda
+                                  or t.numel() < B * self.F * last):
+                raise ValueError(f"{name} must be a contiguous [B, F, {last}] {dt} device tensor")
+        a = _lib.AvzSpectralArgs()
+        a.batch, a.frames = B, T
+        a.Y = Y.data_ptr()
+        a.y_stride_b, a.y_stride_m, a.y_stride_f = Y.stride(0), Y.stride(1), Y.stride(2)
+        a.mask = mask.data_ptr()
+        a.mask_stride_b, a.mask_stride_f = mask.stride(0), mask.stride(1)
+        st = self._steer_ptr(steer)
+        a.steer = st.value if st is not None else None
+        a.S = S.data_ptr()
+        a.s_stride_b, a.s_stride_f = S.stride(0), S.stride(1)
+        a.cov_out = None if cov_out is None else cov_out.data_ptr()
+        a.w_out = None if w_out is None else w_out.data_ptr()
+        fb = self._fallback_ptr(fallback, B)
+        a.fallback = fb.value if fb is not None else None
+        check(lib.avz_beamform_spectral(self._h, ct.byref(a), _stream_handle(stream)),
+              "avz_beamform_spectral")
+        return S
+
+    def istft(self, S: torch.Tensor, *, out=None, peak=None, workspace=None, stream=None):
+        """scipy.signal.istft(S, nperseg=n_fft, noverlap=n_fft/2) of S [B, F, T] complex64
+        (t contiguous): (out [B, >= (T-1) hop], peak [B]); the plan's normalisation applies."""
+        if S.dtype != torch.complex64 or S.dim() != 3 or S.shape[1] != self.F or S.stride(2) != 1 \
+                or not S.is_cuda:
+            raise ValueError(f"S must be complex64 [B, {self.F}, T] (t contiguous) on the device")
+        B, _, T = S.shape
+        n = (T - 1) * self.hop
+        if out is None:
+            out = torch.empty((B, (n + 3) // 4 * 4), dtype=torch.float32, device=S.device)
+        if peak is None:
+            peak = torch.empty((B,), dtype=torch.float32, device=S.device)
+        if out.dtype != torch.float32 or out.dim() != 2 or out.shape[0] < B or out.shape[1] < n \
+                or out.stride(1) != 1:
+            raise ValueError("out must be float32 [>= B, >= (T - 1) hop]")
+        wp, wn = (None, 0) if workspace is None else (ct.c_void_p(workspace.data_ptr()),
+                                                       workspace.numel())
+        check(lib.avz_istft(self._h, B, T, ct.c_void_p(S.data_ptr()), S.stride(0), S.stride(1),
+                            ct.c_void_p(out.data_ptr()), out.stride(0),
+                            ct.c_void_p(peak.data_ptr()), wp, wn, _stream_handle(stream)),
+              "avz_istft")
         return out, peak
 
     def stft(self, x: torch.Tensor, lengths: torch.Tensor | None = None, max_len=None,

@@ -22,6 +22,7 @@ struct Workspace {
   float* heads;
   float* tails;
   uint32_t* peak_u;
+  int* flag;                 // [batch] item-level fallback flags (AVZ_FALLBACK_BATCH)
   float* pf_gain;            // [batch][nchunk][32][F] IRM gains (AVZ_PF_IRM plans only)
 };
 
@@ -47,9 +48,10 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
     w->heads = reinterpret_cast<float*>(q); q += sz_ht;
     w->tails = reinterpret_cast<float*>(q); q += sz_ht;
     w->peak_u = reinterpret_cast<uint32_t*>(q); q += sz_b;
+    w->flag = reinterpret_cast<int*>(q); q += sz_b;
     w->pf_gain = sz_gain ? reinterpret_cast<float*>(q) : nullptr;
   }
-  return sz_part + sz_mw + sz_coef + 2 * sz_ht + sz_b + sz_gain;
+  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 2 * sz_b + sz_gain;
 }
 
 struct avz_plan {
@@ -127,7 +129,8 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
   if ((c.postfilter == AVZ_PF_IBM_TARGET || c.postfilter == AVZ_PF_IRM) &&
       c.mask_mode != AVZ_MASK_IBM)
     return AVZ_ERR_ARG;
-  if (c.singular_fallback != AVZ_FALLBACK_MIC0 && c.singular_fallback != AVZ_FALLBACK_MEAN)
+  if (c.singular_fallback != AVZ_FALLBACK_MIC0 && c.singular_fallback != AVZ_FALLBACK_MEAN &&
+      c.singular_fallback != AVZ_FALLBACK_BATCH)
     return AVZ_ERR_ARG;
   if ((c.postfilter == AVZ_PF_EXT_FLOOR || c.postfilter == AVZ_PF_EXT_MUL) &&
       c.mask_mode != AVZ_MASK_EXTERNAL)
@@ -217,58 +220,9 @@ extern "C" long long avz_mvdr_workspace_bytes(const avz_plan* p, int batch, int 
   return (long long)ws_layout(p->cfg, batch, chunks_for(max_len, p->cfg.hop), nullptr, nullptr);
 }
 
-extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* stream) {
-  if (!p || !a) return AVZ_ERR_ARG;
+// Solve / post-filter parameters of the plan (shared by every chain and spectral call).
+static void plan_params(const avz_plan* p, avz::ChainArgs& k) {
   const avz_config& c = p->cfg;
-  if (a->batch < 0 || a->batch > c.max_batch) return AVZ_ERR_SHAPE;
-  if (a->batch == 0) return AVZ_OK;
-  if (!a->len || !a->mix || !a->out) return AVZ_ERR_ARG;
-  if (a->max_len < c.n_fft || a->max_len > c.max_samples) return AVZ_ERR_SHAPE;
-  if (a->ch_stride < a->max_len) return AVZ_ERR_SHAPE;
-  if (a->batch > 1 && a->mix_stride < a->ch_stride + a->max_len) return AVZ_ERR_SHAPE;
-  const int T = frames_for(a->max_len, c.hop);
-  const int F = c.n_fft / 2 + 1;
-  const long long out_len = (long long)(T - 1) * c.hop;
-  if (a->batch > 1 && a->out_stride < out_len) return AVZ_ERR_SHAPE;
-  if ((a->out_stride & 3) || (reinterpret_cast<uintptr_t>(a->out) & 15)) return AVZ_ERR_ALIGN;
-  if (c.mask_mode == AVZ_MASK_IBM) {
-    if (!a->ref_tgt || !a->ref_int) return AVZ_ERR_ARG;
-    if (a->batch > 1 && a->ref_stride < a->max_len) return AVZ_ERR_SHAPE;
-  }
-  if (c.mask_mode == AVZ_MASK_EXTERNAL) {
-    if (!a->ext_mask) return AVZ_ERR_ARG;
-    // the kernels read M[b][k][t] for every bin and every frame of the longest utterance
-    if (a->mask_bins < F || a->mask_frames < T) return AVZ_ERR_SHAPE;
-  }
-  Workspace ws = p->ws;
-  int nchunk = p->nchunk;
-  if (a->workspace) {
-    nchunk = chunks_for(a->max_len, c.hop);
-    if (reinterpret_cast<uintptr_t>(a->workspace) & 255) return AVZ_ERR_ALIGN;
-    if (a->workspace_bytes < (long long)ws_layout(c, a->batch, nchunk, nullptr, nullptr))
-      return AVZ_ERR_SHAPE;
-    ws_layout(c, a->batch, nchunk, static_cast<char*>(a->workspace), &ws);
-  }
-
-  avz::ChainArgs k{};
-  k.batch = a->batch;
-  k.len = a->len;
-  k.max_len = a->max_len;
-  k.mix = a->mix;
-  k.mix_stride = a->mix_stride;
-  k.ch_stride = a->ch_stride;
-  k.ref_tgt = a->ref_tgt;
-  k.ref_int = a->ref_int;
-  k.ref_stride = a->ref_stride;
-  k.ext_mask = a->ext_mask;
-  k.mask_sb = a->mask_stride_b;
-  k.mask_sf = a->mask_stride_f;
-  k.mask_st = a->mask_stride_t;
-  k.out = a->out;
-  k.out_stride = a->out_stride;
-  k.peak = a->peak;
-  k.cov_out = a->cov_out;
-  k.w_out = a->w_out;
   k.fs = c.fs;
   k.sigma = c.sigma;
   k.tau1 = p->tau1;
@@ -281,17 +235,95 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   k.norm_eps = (float)c.norm_eps;
   k.postfilter = c.postfilter;
   k.normalize = c.normalize;
+  k.singular_fallback = c.singular_fallback;
+  k.beamformer = c.beamformer;
+  k.bypass_hz = c.bypass_hz;
+  k.cond_max = c.cond_max;
+  k.steer = p->steer;
+}
+
+enum { USE_CHAIN = 0, USE_COVARIANCE = 1, USE_APPLY = 2 };
+
+// Validates a time-domain batch call and fills the kernels' argument block: the full
+// chain (avz_mvdr_batch), the covariance stage (refs / mask as the plan's mask mode
+// needs; cov_out required) or the apply + iSTFT stage (mixture only; ext_mask optional).
+static int prepare_chain(const avz_plan* p, const avz_batch_args* a, int use, avz::ChainArgs& k) {
+  if (!p || !a) return AVZ_ERR_ARG;
+  const avz_config& c = p->cfg;
+  if (a->batch < 0 || a->batch > c.max_batch) return AVZ_ERR_SHAPE;
+  if (!a->len || !a->mix || (use != USE_COVARIANCE && !a->out)) return AVZ_ERR_ARG;
+  if (use == USE_COVARIANCE && !a->cov_out) return AVZ_ERR_ARG;
+  if (a->max_len < c.n_fft || a->max_len > c.max_samples) return AVZ_ERR_SHAPE;
+  if (a->ch_stride < a->max_len) return AVZ_ERR_SHAPE;
+  if (a->batch > 1 && a->mix_stride < a->ch_stride + a->max_len) return AVZ_ERR_SHAPE;
+  const int T = frames_for(a->max_len, c.hop);
+  const int F = c.n_fft / 2 + 1;
+  if (use != USE_COVARIANCE) {
+    const long long out_len = (long long)(T - 1) * c.hop;
+    if (a->batch > 1 && a->out_stride < out_len) return AVZ_ERR_SHAPE;
+    if ((a->out_stride & 3) || (reinterpret_cast<uintptr_t>(a->out) & 15)) return AVZ_ERR_ALIGN;
+  }
+  if (use != USE_APPLY && c.mask_mode == AVZ_MASK_IBM) {
+    if (!a->ref_tgt || !a->ref_int) return AVZ_ERR_ARG;
+    if (a->batch > 1 && a->ref_stride < a->max_len) return AVZ_ERR_SHAPE;
+  }
+  const bool needs_mask = use == USE_APPLY ? a->ext_mask != nullptr
+                                           : c.mask_mode == AVZ_MASK_EXTERNAL;
+  if (use != USE_APPLY && c.mask_mode == AVZ_MASK_EXTERNAL && !a->ext_mask) return AVZ_ERR_ARG;
+  // the kernels read M[b][k][t] for every bin and every frame of the longest utterance
+  if (needs_mask && (a->mask_bins < F || a->mask_frames < T)) return AVZ_ERR_SHAPE;
+  Workspace ws = p->ws;
+  int nchunk = p->nchunk;
+  if (a->workspace) {
+    nchunk = chunks_for(a->max_len, c.hop);
+    if (reinterpret_cast<uintptr_t>(a->workspace) & 255) return AVZ_ERR_ALIGN;
+    if (a->workspace_bytes < (long long)ws_layout(c, a->batch, nchunk, nullptr, nullptr))
+      return AVZ_ERR_SHAPE;
+    ws_layout(c, a->batch, nchunk, static_cast<char*>(a->workspace), &ws);
+  }
+  k = avz::ChainArgs{};
+  plan_params(p, k);
+  k.batch = a->batch;
+  k.len = a->len;
+  k.max_len = a->max_len;
+  k.mix = a->mix;
+  k.mix_stride = a->mix_stride;
+  k.ch_stride = a->ch_stride;
+  k.ref_tgt = a->ref_tgt;
+  k.ref_int = a->ref_int;
+  k.ref_stride = a->ref_stride;
+  k.ext_mask = needs_mask ? a->ext_mask : nullptr;
+  k.mask_sb = a->mask_stride_b;
+  k.mask_sf = a->mask_stride_f;
+  k.mask_st = a->mask_stride_t;
+  k.out = a->out;
+  k.out_stride = a->out_stride;
+  k.peak = a->peak;
+  k.cov_out = a->cov_out;
+  k.w_out = a->w_out;
   k.max_frames = T;
   k.nchunk = nchunk;
   k.part = ws.part;
   k.mwords = ws.mwords;
-  k.steer = p->steer;
   k.coef = ws.coef;
   k.heads = ws.heads;
   k.tails = ws.tails;
   k.peak_u = ws.peak_u;
+  k.flag = ws.flag;
   k.pf_gain = ws.pf_gain;
-  k.singular_fallback = c.singular_fallback;
+  return AVZ_OK;
+}
+
+static int hip_rc(int rc) {
+  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  return rc;
+}
+
+extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* stream) {
+  if (p && a && a->batch == 0) return AVZ_OK;
+  avz::ChainArgs k;
+  const int e = prepare_chain(p, a, USE_CHAIN, k);
+  if (e != AVZ_OK) return e;
   avz_plan* mp = const_cast<avz_plan*>(p);  // diagnostic timing state only (not thread-safe)
   void* evs[5];
   int set = -1;
@@ -303,13 +335,128 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
     k.events = evs;
     k.n_events = mp->n_ev;
   }
-  k.beamformer = c.beamformer;
-  k.bypass_hz = c.bypass_hz;
-  k.cond_max = c.cond_max;
-  const int rc = avz_launch_chunked(c.n_fft, c.mask_mode, &k, stream);
-  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  const int rc = hip_rc(avz_launch_chunked(p->cfg.n_fft, p->cfg.mask_mode, &k, stream));
   if (set >= 0 && rc == AVZ_OK) mp->ev_pending[set] = true;
   return rc;
+}
+
+extern "C" int avz_mvdr_covariance(const avz_plan* p, const avz_batch_args* a, void* stream) {
+  if (p && a && a->batch == 0) return AVZ_OK;
+  avz::ChainArgs k;
+  const int e = prepare_chain(p, a, USE_COVARIANCE, k);
+  if (e != AVZ_OK) return e;
+  return hip_rc(avz_launch_covariance(p->cfg.n_fft, p->cfg.mask_mode, &k, stream));
+}
+
+extern "C" int avz_apply_istft(const avz_plan* p, const avz_batch_args* a, const float* w,
+                               void* stream) {
+  if (p && a && a->batch == 0) return AVZ_OK;
+  if (!w || (reinterpret_cast<uintptr_t>(w) & 15)) return w ? AVZ_ERR_ALIGN : AVZ_ERR_ARG;
+  avz::ChainArgs k;
+  const int e = prepare_chain(p, a, USE_APPLY, k);
+  if (e != AVZ_OK) return e;
+  return hip_rc(avz_launch_apply_istft(p->cfg.n_fft, &k, w, stream));
+}
+
+extern "C" int avz_istft(const avz_plan* p, int batch, int frames, const float* S,
+                         long long s_stride_b, long long s_stride_f, float* out,
+                         long long out_stride, float* peak, void* workspace,
+                         long long workspace_bytes, void* stream) {
+  if (!p) return AVZ_ERR_ARG;
+  const avz_config& c = p->cfg;
+  if (batch < 0 || batch > c.max_batch || frames < 0) return AVZ_ERR_SHAPE;
+  if (batch == 0) return AVZ_OK;
+  if (!S || !out) return AVZ_ERR_ARG;
+  const long long len = (long long)(frames - 1) * c.hop;  // scipy.signal.istft output length
+  if (len < c.n_fft || len > c.max_samples) return AVZ_ERR_SHAPE;
+  const int F = c.n_fft / 2 + 1;
+  if (s_stride_f < frames || (batch > 1 && s_stride_b < (long long)F * s_stride_f))
+    return AVZ_ERR_SHAPE;
+  if (batch > 1 && out_stride < len) return AVZ_ERR_SHAPE;
+  if ((out_stride & 3) || (reinterpret_cast<uintptr_t>(out) & 15)) return AVZ_ERR_ALIGN;
+  Workspace ws = p->ws;
+  int nchunk = p->nchunk;
+  if (workspace) {
+    nchunk = chunks_for((int)len, c.hop);
+    if (reinterpret_cast<uintptr_t>(workspace) & 255) return AVZ_ERR_ALIGN;
+    if (workspace_bytes < (long long)ws_layout(c, batch, nchunk, nullptr, nullptr))
+      return AVZ_ERR_SHAPE;
+    ws_layout(c, batch, nchunk, static_cast<char*>(workspace), &ws);
+  }
+  avz::ChainArgs k{};
+  plan_params(p, k);
+  k.postfilter = AVZ_PF_NONE;
+  k.batch = batch;
+  k.len = nullptr;  // every item is (frames - 1) hop samples
+  k.max_len = (int)len;
+  k.max_frames = frames;
+  k.spec = S;
+  k.spec_sb = s_stride_b;
+  k.spec_sf = s_stride_f;
+  k.spec_frames = frames;
+  k.out = out;
+  k.out_stride = out_stride;
+  k.peak = peak;
+  k.nchunk = nchunk;
+  k.heads = ws.heads;
+  k.tails = ws.tails;
+  k.peak_u = ws.peak_u;
+  return hip_rc(avz_launch_istft(c.n_fft, &k, stream));
+}
+
+extern "C" int avz_beamform_spectral(const avz_plan* p, const avz_spectral_args* a, void* stream) {
+  if (!p || !a) return AVZ_ERR_ARG;
+  const avz_config& c = p->cfg;
+  if (a->batch < 0 || a->batch > c.max_batch || a->frames < 1) return AVZ_ERR_SHAPE;
+  if (a->batch == 0) return AVZ_OK;
+  if (!a->Y || !a->mask || !a->S) return AVZ_ERR_ARG;
+  if (c.mask_mode != AVZ_MASK_EXTERNAL) return AVZ_ERR_ARG;  // the mask is a target probability
+  const int F = c.n_fft / 2 + 1;
+  if (a->y_stride_f < a->frames || a->y_stride_m < (long long)F * a->y_stride_f ||
+      a->mask_stride_f < a->frames || a->s_stride_f < a->frames)
+    return AVZ_ERR_SHAPE;
+  if (a->batch > 1 && (a->y_stride_b < 2 * a->y_stride_m ||
+                       a->mask_stride_b < (long long)F * a->mask_stride_f ||
+                       a->s_stride_b < (long long)F * a->s_stride_f))
+    return AVZ_ERR_SHAPE;
+  avz::ChainArgs k{};
+  plan_params(p, k);
+  avz::SpecArgs s{};
+  s.batch = a->batch;
+  s.frames = a->frames;
+  s.Y = a->Y;
+  s.y_sb = a->y_stride_b;
+  s.y_sm = a->y_stride_m;
+  s.y_sf = a->y_stride_f;
+  s.M = a->mask;
+  s.m_sb = a->mask_stride_b;
+  s.m_sf = a->mask_stride_f;
+  s.steer = a->steer ? a->steer : p->steer;
+  s.S = a->S;
+  s.s_sb = a->s_stride_b;
+  s.s_sf = a->s_stride_f;
+  s.cov_out = a->cov_out;
+  s.w_out = a->w_out;
+  s.flag = a->fallback ? a->fallback : p->ws.flag;
+  return hip_rc(avz_launch_spectral(c.n_fft, &s, &k, stream));
+}
+
+extern "C" int avz_solve_covariance(const avz_plan* p, int batch, const double* cov, float* w,
+                                    const double* steer, int* fallback, void* stream) {
+  if (!p) return AVZ_ERR_ARG;
+  if (batch < 0 || batch > p->cfg.max_batch) return AVZ_ERR_SHAPE;
+  if (batch == 0) return AVZ_OK;
+  if (!cov || !w) return AVZ_ERR_ARG;
+  if (reinterpret_cast<uintptr_t>(w) & 15) return AVZ_ERR_ALIGN;
+  avz::ChainArgs k{};
+  plan_params(p, k);
+  avz::SpecArgs s{};
+  s.batch = batch;
+  s.cov_in = cov;
+  s.w_out = w;
+  s.steer = steer ? steer : p->steer;
+  s.flag = fallback ? fallback : p->ws.flag;
+  return hip_rc(avz_launch_solve_cov(p->cfg.n_fft, &s, &k, stream));
 }
 
 extern "C" int avz_plan_set_timing(avz_plan* p, int enable) {

@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "avz_common.hpp"
@@ -109,6 +110,12 @@ __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<
   static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
 }
 
+// Samples of utterance b: the device length clamped to the host-validated max_len (so an
+// inconsistent len[] never moves an access outside the caller's rows), or max_len for all.
+__device__ __forceinline__ int utt_len(const ChainArgs& A, int b) {
+  return A.len ? min(A.len[b], A.max_len) : A.max_len;
+}
+
 // Mask value m and covariance weight of one (bin, frame).
 template <int MASK>
 __device__ __forceinline__ float bin_mask(const ChainArgs& A, int b, cf x0, cf x1, cf zr,
@@ -160,7 +167,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
-  const int L = min(A.len[b], A.max_len);  // a device length never exceeds the rows
+  const int L = utt_len(A, b);
   if (L < N) return;  // host validates; finalize reports NaN for a bad device length
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
@@ -437,7 +444,7 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
   if (idx >= (long long)A.batch * F) return;
   const int b = (int)(idx / F), k = (int)(idx % F);
-  const int L = min(A.len[b], A.max_len);  // a device length never exceeds the rows
+  const int L = utt_len(A, b);
   if (L < N) return;
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
@@ -449,18 +456,44 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) R[q] *= 0.25;  // analysis accumulates (2 y)(2 y)^H
+  if (A.cov_only) {  // covariance stage export
+#pragma unroll
+    for (int q = 0; q < 5; ++q) A.cov_out[((long long)b * F + k) * 5 + q] = R[q];
+    return;
+  }
   const double* d = A.steer + 4 * k;
   cf al, be;
   float* wdbg = A.w_out ? A.w_out + ((long long)b * F + k) * 4 : nullptr;
-  if (A.beamformer == BF_HYBRID_NULL)
+  if (A.beamformer == BF_HYBRID_NULL) {
     hybrid_solve_d(R, k, N, A, d[0], d[1], d[2], d[3], al, be, wdbg);
-  else
-    mvdr_solve_d(R, k, N, A, d[0], d[1], d[2], d[3], al, be, wdbg);
+  } else {
+    double w[4];
+    bool sing = false;
+    mvdr_weights_d(R, k, N, A, d[0], d[1], d[2], d[3], w, &sing);
+    if (sing && A.singular_fallback == 2) atomicOr(A.flag + b, 1);  // item-level fallback
+    coef_from_w(w[0], w[1], w[2], w[3], al, be, wdbg);
+  }
   reinterpret_cast<float4*>(A.coef)[(long long)b * F + k] = make_float4(al.x, al.y, be.x, be.y);
   if (A.cov_out) {
 #pragma unroll
     for (int q = 0; q < 5; ++q) A.cov_out[((long long)b * F + k) * 5 + q] = R[q];
   }
+}
+
+// batch_mvdr's item-level fallback (AVZ_FALLBACK_BATCH): the items whose solve met a
+// singular bin get w = [1 / (conj(d0) + 1e-10), 0] on every bin. No-op otherwise.
+template <int N>
+__global__ void __launch_bounds__(kSolveThreads) avz_solve_fixup_kernel(ChainArgs A) {
+  constexpr int F = N / 2 + 1;
+  const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
+  if (idx >= (long long)A.batch * F) return;
+  const int b = (int)(idx / F), k = (int)(idx % F);
+  if (A.flag[b] == 0) return;
+  double w[4];
+  batch_fallback_weights_d(A.steer[4 * k], A.steer[4 * k + 1], w);
+  cf al, be;
+  coef_from_w(w[0], w[1], w[2], w[3], al, be, A.w_out ? A.w_out + idx * 4 : nullptr);
+  reinterpret_cast<float4*>(A.coef)[idx] = make_float4(al.x, al.y, be.x, be.y);
 }
 
 // ================================ SRP scan ================================
@@ -476,7 +509,7 @@ __global__ void __launch_bounds__(kSrpThreads) avz_srp_kernel(ChainArgs A, SrpAr
   __shared__ double R[F][4];
   __shared__ double red[kSrpThreads / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int L = min(A.len[b], A.max_len);  // a device length never exceeds the rows
+  const int L = utt_len(A, b);
   double* out = S.power_db + (long long)b * S.n_angles;
   if (L < N) {
     for (int i = tid; i < S.n_angles; i += kSrpThreads) out[i] = __builtin_nan("");
@@ -527,9 +560,12 @@ __global__ void __launch_bounds__(kSrpThreads) avz_srp_kernel(ChainArgs A, SrpAr
 }
 
 // ================================ synthesis ================================
-template <int N, int PF>
+// SPEC: the frames' spectra come from A.spec (avz_istft: scipy.signal.istft of a given
+// S[b][k][t]) instead of the forward FFT of the mixture and the apply step.
+template <int N, int PF, bool SPEC>
 __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char* lds, int c,
                                                int b) {
+  static_assert(!SPEC || PF == PF_NONE, "spectrum input carries its own post-filter");
   using C = KCfg<N>;
   using G = CGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
@@ -545,7 +581,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
-  const int L = min(A.len[b], A.max_len);  // a device length never exceeds the rows
+  const int L = utt_len(A, b);
   if (L < N) return;
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
@@ -581,7 +617,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   };
   AVZ_STAMP_DECL();
   AVZ_STAMP_INIT();
-  issue_loads(0);
+  if constexpr (!SPEC) issue_loads(0);
 
   // ---- apply coefficients and post-filter bits of this thread's bins
   const float4* coef = reinterpret_cast<const float4*>(A.coef) + (long long)b * F;
@@ -590,7 +626,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   uint32_t bits[BPT];
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
-    const float4 cw = coef[tid + j * NT];
+    const float4 cw = SPEC ? make_float4(0.f, 0.f, 0.f, 0.f) : coef[tid + j * NT];
     alpha[j] = cf{cw.x, cw.y};
     beta[j] = cf{cw.z, cw.w};
     bits[j] = (PF == PF_IBM_TARGET) ? MW[tid + j * NT] : 0u;
@@ -598,7 +634,13 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   const bool nyq_wave = (wave == G::NWAVE - 1);
   cf alpha_n{0, 0}, beta_n{0, 0};
   uint32_t bits_n = 0u;
-  if (nyq_wave) {
+  // spectrum input: S[b][k][t] rows (t contiguous); frames past spec_frames read as zero
+  const float2* Sb = SPEC ? reinterpret_cast<const float2*>(A.spec) + (long long)b * A.spec_sb
+                          : nullptr;
+  const int TS = SPEC ? min(T, A.spec_frames) : T;
+  const bool svec = SPEC && ((A.spec_sb | A.spec_sf) & 1) == 0 &&
+                    ((reinterpret_cast<uintptr_t>(A.spec) & 15) == 0);
+  if (nyq_wave && !SPEC) {
     const float4 cw = coef[N / 2];
     alpha_n = cf{cw.x, cw.y};
     beta_n = cf{cw.z, cw.w};
@@ -651,10 +693,12 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     AVZ_STAMP(5);
 #endif
-    window_fft<N>(v, wc, fft, my_spec, twid, lm);
-    // x2: the next step's loads fly through apply, inverse FFT and OLA; x1 issues them
-    // after the inverse FFT (its registers are needed there at four waves per SIMD)
-    if (!AVZ_X1 && more) issue_loads(step + 1);
+    if constexpr (!SPEC) {
+      window_fft<N>(v, wc, fft, my_spec, twid, lm);
+      // x2: the next step's loads fly through apply, inverse FFT and OLA; x1 issues them
+      // after the inverse FFT (its registers are needed there at four waves per SIMD)
+      if (!AVZ_X1 && more) issue_loads(step + 1);
+    }
     lds_barrier();
     AVZ_STAMP(6);
 
@@ -716,7 +760,44 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       }
     }
     };
-    if constexpr (PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) {
+    // spectrum input: the step's frames of the thread's bins straight from S, packed as
+    // above (16-B row segments when the rows are aligned and the step is complete)
+    auto spec_phase = [&](auto vec) {
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) {
+        const int kb = tid + j * NT;
+        const int kp = (N - kb) & (N - 1);
+        const float2* row = Sb + (long long)kb * A.spec_sf + f0;
+        cf sv[FB];
+        if constexpr (decltype(vec)::value) {
+#pragma unroll
+          for (int q = 0; q < FB / 2; ++q) {
+            const float4 x = reinterpret_cast<const float4*>(row)[q];
+            sv[2 * q] = cf{x.x, x.y};
+            sv[2 * q + 1] = cf{x.z, x.w};
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < FB; ++i) {
+            const float2 x = (f0 + i < TS) ? row[i] : make_float2(0.f, 0.f);
+            sv[i] = cf{x.x, x.y};
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < NPAIR; ++p) {
+          cf* Za = slot_ptr<N>(lds, 2 * p);
+          const cf sa = sv[2 * p], sb = sv[2 * p + 1];
+          Za[kp] = {sa.x + sb.y, sb.x - sa.y};
+          Za[kb] = (kb == 0) ? cf{sa.x, sb.x} : cf{sa.x - sb.y, sa.y + sb.x};
+        }
+      }
+    };
+    if constexpr (SPEC) {
+      if (svec && f0 + FB <= TS)  // block-uniform
+        spec_phase(std::true_type{});
+      else
+        spec_phase(std::false_type{});
+    } else if constexpr (PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) {
       if (mask_vec && f0 + FB <= T)  // wave-uniform
         apply_phase(std::true_type{});
       else
@@ -724,7 +805,15 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     } else {
       apply_phase(std::false_type{});
     }
-    if (nyq_wave && lane < NPAIR) {  // Nyquist bin: frame pair `lane`
+    if (SPEC && nyq_wave && lane < NPAIR) {  // Nyquist bin from S: real parts (irfft)
+      const int ta = f0 + 2 * lane;
+      if (ta < T) {
+        const float2* row = Sb + (long long)(N / 2) * A.spec_sf;
+        const float xa = ta < TS ? row[ta].x : 0.f, xb = ta + 1 < TS ? row[ta + 1].x : 0.f;
+        slot_ptr<N>(lds, 2 * lane)[N / 2] = {xa, xb};
+      }
+    }
+    if (!SPEC && nyq_wave && lane < NPAIR) {  // Nyquist bin: frame pair `lane`
       const int ta = f0 + 2 * lane;
       if (ta < T) {
         const int ia = step * FB + 2 * lane;
@@ -842,7 +931,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
 }
 
 // Persistent grid over (chunk, utterance) items, as avz_analysis_kernel.
-template <int N, int PF>
+template <int N, int PF, bool SPEC = false>
 __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_synthesis_kernel(ChainArgs A) {
   using G = CGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -850,7 +939,7 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_syn
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
   const int n_items = gx * A.batch;
   for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-    synthesis_item<N, PF>(A, lds, it % gx, it / gx);
+    synthesis_item<N, PF, SPEC>(A, lds, it % gx, it / gx);
 }
 
 // ================================ finalize ================================
@@ -860,7 +949,7 @@ __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
   __shared__ float red[NWAVE];
   const int c = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int L = min(A.len[b], A.max_len);  // a device length never exceeds the rows
+  const int L = utt_len(A, b);
   if (L < N) {
     if (c == 0 && tid == 0 && A.peak) A.peak[b] = __builtin_nanf("");
     return;
@@ -914,24 +1003,26 @@ extern "C" int avz_debug_set_stamps_chunked(void* dev_ptr) {
 }
 #endif
 
-// Compute units of the current device (cached per process; one device per process here).
+// Compute units of the current device (cached per device id; thread-safe).
 static int resident_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-      n = v;
-    else
-      n = 256;
-  }
-  return n;
+  static std::atomic<int> cache[64];
+  int dev = 0, v = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+  if (dev < 64 && cache[dev].load(std::memory_order_relaxed) > 0)
+    return cache[dev].load(std::memory_order_relaxed);
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+    v = 256;
+  if (dev < 64) cache[dev].store(v, std::memory_order_relaxed);
+  return v;
 }
 
-template <typename K>
-static bool set_lds(K kern, int lds) {
-  return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) ==
-         hipSuccess;
+// Dynamic-LDS attribute of one kernel, set once (thread-safe static initialisation).
+template <auto Kern>
+static bool lds_ready(int lds) {
+  static const bool ok = hipFuncSetAttribute((const void*)Kern,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             lds) == hipSuccess;
+  return ok;
 }
 
 template <int N, int MASK, int PF>
@@ -941,11 +1032,9 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   auto k3 = avz_finalize_kernel<N>;
   auto ks = avz_solve_kernel<N>;
   constexpr int lds = CGeo<N>::LDS_BYTES;
-  static bool attr_done = false;
-  if (!attr_done) {
-    if (!set_lds(k1, lds) || !set_lds(k2, lds)) return -3;
-    attr_done = true;
-  }
+  if (!lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM>>(lds) ||
+      !lds_ready<avz_synthesis_kernel<N, PF>>(lds))
+    return -3;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
   const dim3 grid(nch, a->batch);
@@ -957,10 +1046,15 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   auto mark = [&](int i) {
     if (ev && i < a->n_events) (void)hipEventRecord(ev[i], st);
   };
+  const bool item_fallback = a->singular_fallback == 2 && a->beamformer == BF_MVDR;
+  if (item_fallback && hipMemsetAsync(a->flag, 0, sizeof(int) * a->batch, st) != hipSuccess)
+    return -3;
   mark(0);
   hipLaunchKernelGGL(k1, pgrid, dim3(kCThreads), lds, st, *a);
   mark(1);
   hipLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, *a);
+  if (item_fallback)
+    hipLaunchKernelGGL(avz_solve_fixup_kernel<N>, dim3(nsolve), dim3(kSolveThreads), 0, st, *a);
   mark(2);
   const dim3 sgrid((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus()));
   hipLaunchKernelGGL(k2, sgrid, dim3(kCThreads), lds, st, *a);
@@ -988,11 +1082,7 @@ template <int N>
 static int launch_srp_t(const ChainArgs* a, const SrpArgs* s, hipStream_t st) {
   auto k1 = avz_analysis_kernel<N, MASK_ONES, false>;
   constexpr int lds = CGeo<N>::LDS_BYTES;
-  static bool attr_done = false;
-  if (!attr_done) {
-    if (!set_lds(k1, lds)) return -3;
-    attr_done = true;
-  }
+  if (!lds_ready<avz_analysis_kernel<N, MASK_ONES, false>>(lds)) return -3;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
   const int n_items = nch * a->batch;
@@ -1027,5 +1117,87 @@ extern "C" int avz_launch_chunked(int n_fft, int mask_mode, const ChainArgs* a, 
       case MASK_ONES: return launch_pf<512, MASK_ONES>(a, st);
     }
   }
+  return -4;
+}
+
+// ================================ stage exports ================================
+// Apply coefficients of caller weights w[b][k] = (Re w0, Im w0, Re w1, Im w1) (the w_out
+// layout): S = conj(w0) y0 + conj(w1) y1 as alpha Z[k] + beta conj(Z[N-k]).
+__global__ void __launch_bounds__(256) avz_coef_kernel(ChainArgs A, const float* w, int F) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)A.batch * F) return;
+  const float4 x = reinterpret_cast<const float4*>(w)[i];
+  cf al, be;
+  coef_from_w(x.x, x.y, x.z, x.w, al, be, nullptr);
+  reinterpret_cast<float4*>(A.coef)[i] = make_float4(al.x, al.y, be.x, be.y);
+}
+
+template <int N, int MASK>
+static int launch_cov_t(const ChainArgs* a, hipStream_t st) {
+  constexpr int lds = CGeo<N>::LDS_BYTES;
+  if (!lds_ready<avz_analysis_kernel<N, MASK, false>>(lds)) return -3;
+  const int nch = (a->max_frames + kChunk - 1) / kChunk;
+  if (nch > a->nchunk) return -2;
+  const int n_items = nch * a->batch;
+  ChainArgs c = *a;
+  c.cov_only = 1;
+  hipLaunchKernelGGL((avz_analysis_kernel<N, MASK, false>),
+                     dim3((unsigned)std::min(n_items, CGeo<N>::BLOCKS * resident_cus())),
+                     dim3(kCThreads), lds, st, c);
+  constexpr int F = N / 2 + 1;
+  const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
+  hipLaunchKernelGGL(avz_solve_kernel<N>, dim3(nsolve), dim3(kSolveThreads), 0, st, c);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int avz_launch_covariance(int n_fft, int mask_mode, const ChainArgs* a, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (a->batch <= 0) return 0;
+#define AVZ_COV_CASES(NN)                                                   \
+  switch (mask_mode) {                                                      \
+    case MASK_IBM: return launch_cov_t<NN, MASK_IBM>(a, st);                \
+    case MASK_IPD: return launch_cov_t<NN, MASK_IPD>(a, st);                \
+    case MASK_EXTERNAL: return launch_cov_t<NN, MASK_EXTERNAL>(a, st);      \
+    case MASK_ONES: return launch_cov_t<NN, MASK_ONES>(a, st);              \
+  }
+  if (n_fft == 1024) { AVZ_COV_CASES(1024) }
+  if (n_fft == 512) { AVZ_COV_CASES(512) }
+#undef AVZ_COV_CASES
+  return -4;
+}
+
+template <int N, int PF, bool SPEC>
+static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
+  constexpr int lds = CGeo<N>::LDS_BYTES;
+  if (!lds_ready<avz_synthesis_kernel<N, PF, SPEC>>(lds)) return -3;
+  const int nch = (a->max_frames + kChunk - 1) / kChunk;
+  if (nch > a->nchunk) return -2;
+  const int n_items = nch * a->batch;
+  hipLaunchKernelGGL((avz_synthesis_kernel<N, PF, SPEC>),
+                     dim3((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus())),
+                     dim3(kCThreads), lds, st, *a);
+  hipLaunchKernelGGL(avz_finalize_kernel<N>, dim3(nch, a->batch), dim3(kCThreads), 0, st, *a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int avz_launch_apply_istft(int n_fft, const ChainArgs* a, const float* w, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (a->batch <= 0) return 0;
+  const int F = n_fft / 2 + 1;
+  const long long n = (long long)a->batch * F;
+  hipLaunchKernelGGL(avz_coef_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *a, w, F);
+  const bool g = a->ext_mask != nullptr;
+  if (n_fft == 1024)
+    return g ? launch_synth_t<1024, PF_EXT_MUL, false>(a, st) : launch_synth_t<1024, PF_NONE, false>(a, st);
+  if (n_fft == 512)
+    return g ? launch_synth_t<512, PF_EXT_MUL, false>(a, st) : launch_synth_t<512, PF_NONE, false>(a, st);
+  return -4;
+}
+
+extern "C" int avz_launch_istft(int n_fft, const ChainArgs* a, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (a->batch <= 0) return 0;
+  if (n_fft == 1024) return launch_synth_t<1024, PF_NONE, true>(a, st);
+  if (n_fft == 512) return launch_synth_t<512, PF_NONE, true>(a, st);
   return -4;
 }

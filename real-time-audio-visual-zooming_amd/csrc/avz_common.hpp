@@ -250,15 +250,16 @@ __device__ __forceinline__ void coef_from_w(double w0r, double w0i, double w1r, 
   }
 }
 
-// Per-bin MVDR solve in fp64 (oracle_debug.py:66-79):
+// Per-bin MVDR weights in fp64 (oracle_debug.py:66-79):
 //   w~ = (R/(sum m + 1e-6) + sigma I)^{-1} d ; w = w~ / (d^H w~ + 1e-10);
 //   singular -> w = [1, 0] (or ones/2, oracle_reverb.py:133-135); f < fmin -> w = 0.
 // d = steering vector (masked_mvdr.py:22-35). c = {sum m|y0|^2, sum m|y1|^2,
-// Re/Im sum m y0 conj(y1), sum m}.
-__device__ __forceinline__ void mvdr_solve_d(const double (&c)[5], int k, int n_fft,
-                                             const ChainArgs& A, double d0r, double d0i,
-                                             double d1r, double d1i, cf& alpha, cf& beta,
-                                             float* w_dbg) {
+// Re/Im sum m y0 conj(y1), sum m}. w = {Re w0, Im w0, Re w1, Im w1}. *singular is set
+// when the loaded covariance is exactly singular (whatever the fallback policy).
+__device__ __forceinline__ void mvdr_weights_d(const double (&c)[5], int k, int n_fft,
+                                               const ChainArgs& A, double d0r, double d0i,
+                                               double d1r, double d1i, double (&w)[4],
+                                               bool* singular) {
   double w0r = 0, w0i = 0, w1r = 0, w1i = 0;
   const double fk = (double)k * A.fs / (double)n_fft;
   if (!(fk < A.fmin_hz)) {
@@ -266,20 +267,29 @@ __device__ __forceinline__ void mvdr_solve_d(const double (&c)[5], int k, int n_
     const double a = c[0] / nrm + A.sigma, e = c[1] / nrm + A.sigma;
     const double br = c[2] / nrm, bi = c[3] / nrm;
     const double det = a * e - (br * br + bi * bi);
+    double t0r, t0i, t1r, t1i;
+    bool solved = true;
     if (det == 0.0 || !isfinite(det)) {
-      if (A.singular_fallback) {  // oracle_reverb.py:133-135: ones(n)/n
+      if (singular) *singular = (det == 0.0);
+      if (A.singular_fallback == 1) {  // oracle_reverb.py:133-135: ones(n)/n, not normalised
         w0r = 0.5;
         w1r = 0.5;
-      } else {  // oracle_debug.py:78-79: [1, 0]
+        solved = false;
+      } else if (A.singular_fallback == 0) {  // oracle_debug.py:78-79: [1, 0], not normalised
         w0r = 1.0;
+        solved = false;
+      } else {  // batch_mvdr (tf_lite_version/inference.py:143-157): w~ = [1, 0], normalised
+        t0r = 1.0; t0i = 0.0; t1r = 0.0; t1i = 0.0;
       }
     } else {
       // w~0 = (e d0 - b d1)/det ; w~1 = (a d1 - conj(b) d0)/det
-      double t0r = e * d0r - (br * d1r - bi * d1i);
-      double t0i = e * d0i - (br * d1i + bi * d1r);
-      double t1r = a * d1r - (br * d0r + bi * d0i);
-      double t1i = a * d1i - (br * d0i - bi * d0r);
+      t0r = e * d0r - (br * d1r - bi * d1i);
+      t0i = e * d0i - (br * d1i + bi * d1r);
+      t1r = a * d1r - (br * d0r + bi * d0i);
+      t1i = a * d1i - (br * d0i - bi * d0r);
       t0r /= det; t0i /= det; t1r /= det; t1i /= det;
+    }
+    if (solved) {
       // den = conj(d0) w~0 + conj(d1) w~1 + 1e-10
       const double dr = d0r * t0r + d0i * t0i + d1r * t1r + d1i * t1i + 1e-10;
       const double di = d0r * t0i - d0i * t0r + d1r * t1i - d1i * t1r;
@@ -290,7 +300,28 @@ __device__ __forceinline__ void mvdr_solve_d(const double (&c)[5], int k, int n_
       w1i = (t1i * dr - t1r * di) / dd;
     }
   }
-  coef_from_w(w0r, w0i, w1r, w1i, alpha, beta, w_dbg);
+  w[0] = w0r; w[1] = w0i; w[2] = w1r; w[3] = w1i;
+}
+
+// batch_mvdr's item-level fallback weights (tf_lite_version/inference.py:149-157): every
+// bin w~ = [1, 0]^T, normalised: w = [1 / (conj(d0) + 1e-10), 0].
+__device__ __forceinline__ void batch_fallback_weights_d(double d0r, double d0i,
+                                                         double (&w)[4]) {
+  const double dr = d0r + 1e-10, di = -d0i;  // conj(d0) + 1e-10
+  const double dd = dr * dr + di * di;
+  w[0] = dr / dd;
+  w[1] = -di / dd;
+  w[2] = 0.0;
+  w[3] = 0.0;
+}
+
+__device__ __forceinline__ void mvdr_solve_d(const double (&c)[5], int k, int n_fft,
+                                             const ChainArgs& A, double d0r, double d0i,
+                                             double d1r, double d1i, cf& alpha, cf& beta,
+                                             float* w_dbg) {
+  double w[4];
+  mvdr_weights_d(c, k, n_fft, A, d0r, d0i, d1r, d1i, w, nullptr);
+  coef_from_w(w[0], w[1], w[2], w[3], alpha, beta, w_dbg);
 }
 
 // Per-bin hybrid hard-null weights in fp64 (Final_pipeline/src/inference.py:28-98):
@@ -303,13 +334,12 @@ __device__ __forceinline__ void mvdr_solve_d(const double (&c)[5], int k, int n_
 // Where the reference's eigenvector has v_int[0] == 0 (R diagonal with R11 >= R00, e.g.
 // no noise-weighted frames) it divides by zero and np.linalg.cond then raises; here
 // that bin takes the delay-and-sum fallback.
-__device__ __forceinline__ void hybrid_solve_d(const double (&c)[5], int k, int n_fft,
-                                               const ChainArgs& A, double t0r, double t0i,
-                                               double t1r, double t1i, cf& alpha, cf& beta,
-                                               float* w_dbg) {
+__device__ __forceinline__ void hybrid_weights_d(const double (&c)[5], int k, int n_fft,
+                                                 const ChainArgs& A, double t0r, double t0i,
+                                                 double t1r, double t1i, double (&w)[4]) {
   const double fk = (double)k * A.fs / (double)n_fft;
   if (fk < A.bypass_hz) {
-    coef_from_w(1.0, 0.0, 0.0, 0.0, alpha, beta, w_dbg);
+    w[0] = 1.0; w[1] = 0.0; w[2] = 0.0; w[3] = 0.0;
     return;
   }
   const double nrm = c[4] + 1e-6;
@@ -357,7 +387,16 @@ __device__ __forceinline__ void hybrid_solve_d(const double (&c)[5], int k, int 
       w1i = -(v0r * ii - v0i * ir);
     }
   }
-  coef_from_w(w0r, w0i, w1r, w1i, alpha, beta, w_dbg);
+  w[0] = w0r; w[1] = w0i; w[2] = w1r; w[3] = w1i;
+}
+
+__device__ __forceinline__ void hybrid_solve_d(const double (&c)[5], int k, int n_fft,
+                                               const ChainArgs& A, double t0r, double t0i,
+                                               double t1r, double t1i, cf& alpha, cf& beta,
+                                               float* w_dbg) {
+  double w[4];
+  hybrid_weights_d(c, k, n_fft, A, t0r, t0i, t1r, t1i, w);
+  coef_from_w(w[0], w[1], w[2], w[3], alpha, beta, w_dbg);
 }
 
 __device__ __forceinline__ cf apply_bin(cf alpha, cf beta, cf z, cf zp, float g) {

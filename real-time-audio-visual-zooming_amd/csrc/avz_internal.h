@@ -46,8 +46,34 @@ struct ChainArgs {
   uint32_t* peak_u;           // [B] max |out| over chunk interiors (float bits, atomicMax)
   float* pf_gain;             // [B][nchunk][32][F] IRM post-filter gain (PF_IRM) or null
   int singular_fallback;      // 0: w = [1, 0]; 1: w = [1/2, 1/2]
+  // spectrum-input synthesis (avz_istft): S[b][k][t] complex64 replaces the forward FFT of
+  // the mixture and the apply step (post-filter still applied); len == null means every
+  // utterance is max_len samples long
+  const float* spec;
+  long long spec_sb, spec_sf; // complex elements; t stride 1
+  int spec_frames;            // frames present in S (frames >= spec_frames read as zero)
+  int cov_only;               // solve kernel: write cov_out only (the covariance stage export)
+  int* flag;                  // [B] item-level (batch_mvdr) fallback flags, zeroed per call
   void* const* events;        // host-only: 5 hipEvent_t recorded around the 4 launches, or null
   int n_events;               // host-only: how many of them to record (5, or 2: analysis only)
+};
+
+// Spectral-domain beamformer (avz_beamform_spectral) and the solve stage export
+// (avz_solve_covariance). Solve parameters come from a ChainArgs (fs, sigma, fmin_hz,
+// weight_eps, singular_fallback, bypass_hz, cond_max, postfilter, pf_floor).
+struct SpecArgs {
+  int batch, frames;
+  const float* Y;             // complex64 Y[b][m][k][t], m = 0, 1 (t contiguous)
+  long long y_sb, y_sm, y_sf; // complex elements
+  const float* M;             // target probability M[b][k][t] (t contiguous)
+  long long m_sb, m_sf;
+  const double* steer;        // [F][4] d0 (re, im), d1 (re, im)
+  float* S;                   // complex64 S[b][k][t] (t contiguous)
+  long long s_sb, s_sf;
+  double* cov_out;            // [B][F][5] or null
+  float* w_out;               // [B][F][4] or null
+  const double* cov_in;       // solve stage: [B][F][5] covariance sums
+  int* flag;                  // [B] item-level fallback flags (zeroed by the launcher)
 };
 
 struct StftArgs {
@@ -130,6 +156,14 @@ int avz_launch_chunk_split(const avz::ChunkSplitArgs* a, void* stream);
 int avz_launch_metrics(const avz::MetricsArgs* a, void* stream);
 int avz_launch_chunk_merge(const avz::ChunkMergeArgs* a, void* stream);
 int avz_launch_chunked(int n_fft, int mask_mode, const avz::ChainArgs* a, void* stream);
+// stage exports: analysis + partial sums -> cov_out; w [B][F][4] -> coef -> synthesis +
+// finalize (post-filter PF_NONE or PF_EXT_MUL with ext_mask as the gain); S -> synthesis
+// (spectrum input) + finalize
+int avz_launch_covariance(int n_fft, int mask_mode, const avz::ChainArgs* a, void* stream);
+int avz_launch_apply_istft(int n_fft, const avz::ChainArgs* a, const float* w, void* stream);
+int avz_launch_istft(int n_fft, const avz::ChainArgs* a, void* stream);
+int avz_launch_spectral(int n_fft, const avz::SpecArgs* s, const avz::ChainArgs* p, void* stream);
+int avz_launch_solve_cov(int n_fft, const avz::SpecArgs* s, const avz::ChainArgs* p, void* stream);
 int avz_launch_srp(int n_fft, const avz::ChainArgs* a, const avz::SrpArgs* s, void* stream);
 int avz_chunk_frames(void);
 int avz_launch_stft(int n_fft, const avz::StftArgs* a, void* stream);

@@ -1,0 +1,219 @@
+// avz_spectral.hip — spectral-domain beamformers for callers that already hold an STFT
+// (gfx950), and the solve-from-covariance stage export.
+//
+//  * batch_mvdr(Y[M,F,T], mask[F,T], f_bins, d_vectors, sigma) -> S[F,T]
+//    (rt_av_zoom/core/tf_lite_version/inference.py:85-179): covariance weighted by
+//    sqrt(1 - mask + 1e-10) (so 1 - mask + 1e-10 on R), normalised by sum(1 - mask) + 1e-6,
+//    + sigma I, no low-frequency skip, w = R^-1 d / (d^H R^-1 d + 1e-10), S = w^H y; one
+//    np.linalg.solve over all bins, so a singular bin sends EVERY bin of the call to the
+//    fallback w~ = [1, 0]^T (then normalised) — AVZ_FALLBACK_BATCH.
+//  * hybrid_hard_null_bf(Y, mask, f_bins) -> S (Final_pipeline/src/inference.py:28-98):
+//    f < 200 Hz passes mic 0; else the hard null of hybrid_weights_d.
+//
+// Layout: one wave per (item, bin) row, frames across lanes (t contiguous, so every load
+// and store instruction moves 256-512 contiguous bytes); the masked 2x2 covariance is
+// accumulated per lane in fp64 and reduced across the wave, every lane solves the same
+// fp64 2x2 (wave-uniform), and the row is re-read (L1/L2 hit) for the apply. HBM-bound:
+// 2 x 8 B (Y) + 4 B (mask) + 8 B (S) = 28 B per TF-bin. An optional post-filter gain from
+// the same mask (x max(M, floor) / x M) is fused into the store.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "avz_common.hpp"
+
+namespace avz {
+
+constexpr int kSpecThreads = 256;  // 4 waves = 4 rows per block
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int PF>
+__device__ __forceinline__ float spec_gain(const ChainArgs& P, float M) {
+  if constexpr (PF == PF_EXT_FLOOR) return fmaxf(M, P.pf_floor);
+  else if constexpr (PF == PF_EXT_MUL) return M;
+  else return 1.0f;
+}
+
+// S[t] = gain(M[t]) * (conj(w0) y0[t] + conj(w1) y1[t]) over the row's frames.
+template <int PF>
+__device__ __forceinline__ void spec_apply_row(const SpecArgs& S, const ChainArgs& P,
+                                               const float2* y0, const float2* y1,
+                                               const float* m, float2* out,
+                                               const double (&w)[4], int lane) {
+  for (int t = lane; t < S.frames; t += 64) {
+    const float2 a = y0[t], e = y1[t];
+    const double sr = w[0] * a.x + w[1] * a.y + w[2] * e.x + w[3] * e.y;
+    const double si = w[0] * a.y - w[1] * a.x + w[2] * e.y - w[3] * e.x;
+    const float g = spec_gain<PF>(P, m[t]);
+    out[t] = make_float2((float)sr * g, (float)si * g);
+  }
+}
+
+template <int N, bool HYB, int PF>
+__global__ void __launch_bounds__(kSpecThreads) avz_spectral_kernel(SpecArgs S, ChainArgs P) {
+  constexpr int F = N / 2 + 1;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * (kSpecThreads / 64) + wave;
+  if (row >= (long long)S.batch * F) return;
+  const int b = (int)(row / F), k = (int)(row % F);
+  const float2* y0 = reinterpret_cast<const float2*>(S.Y) + b * S.y_sb + k * S.y_sf;
+  const float2* y1 = y0 + S.y_sm;
+  const float* m = S.M + b * S.m_sb + k * S.m_sf;
+  double c[5] = {0, 0, 0, 0, 0};
+  for (int t = lane; t < S.frames; t += 64) {
+    const float2 a = y0[t], e = y1[t];
+    const float mn = 1.0f - m[t];  // float32, as numpy's 1.0 - (float32 mask)
+    const double wg = (double)mn + P.weight_eps;
+    const double ar = a.x, ai = a.y, er = e.x, ei = e.y;
+    c[0] = fma(wg, ar * ar + ai * ai, c[0]);
+    c[1] = fma(wg, er * er + ei * ei, c[1]);
+    c[2] = fma(wg, ar * er + ai * ei, c[2]);  // Re y0 conj(y1)
+    c[3] = fma(wg, ai * er - ar * ei, c[3]);  // Im y0 conj(y1)
+    c[4] += (double)mn;
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) c[q] = wave_sum_d(c[q]);
+  const double* d = S.steer + 4 * k;
+  double w[4];
+  if constexpr (HYB) {
+    hybrid_weights_d(c, k, N, P, d[0], d[1], d[2], d[3], w);
+  } else {
+    bool sing = false;
+    mvdr_weights_d(c, k, N, P, d[0], d[1], d[2], d[3], w, &sing);
+    if (sing && P.singular_fallback == 2 && lane == 0) atomicOr(S.flag + b, 1);
+  }
+  if (lane == 0) {
+    if (S.cov_out) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) S.cov_out[row * 5 + q] = c[q];
+    }
+    if (S.w_out) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) S.w_out[row * 4 + q] = (float)w[q];
+    }
+  }
+  spec_apply_row<PF>(S, P, y0, y1, m, reinterpret_cast<float2*>(S.S) + b * S.s_sb + k * S.s_sf,
+                     w, lane);
+}
+
+// batch_mvdr's fallback for the items whose solve met a singular bin: every bin of the
+// item is redone with w~ = [1, 0]^T (normalised). A no-op for every other item.
+template <int N, int PF>
+__global__ void __launch_bounds__(kSpecThreads) avz_spectral_fixup_kernel(SpecArgs S, ChainArgs P) {
+  constexpr int F = N / 2 + 1;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * (kSpecThreads / 64) + wave;
+  if (row >= (long long)S.batch * F) return;
+  const int b = (int)(row / F), k = (int)(row % F);
+  if (S.flag[b] == 0) return;
+  double w[4];
+  batch_fallback_weights_d(S.steer[4 * k], S.steer[4 * k + 1], w);
+  if (lane == 0 && S.w_out) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S.w_out[row * 4 + q] = (float)w[q];
+  }
+  const float2* y0 = reinterpret_cast<const float2*>(S.Y) + b * S.y_sb + k * S.y_sf;
+  spec_apply_row<PF>(S, P, y0, y0 + S.y_sm, S.M + b * S.m_sb + k * S.m_sf,
+                     reinterpret_cast<float2*>(S.S) + b * S.s_sb + k * S.s_sf, w, lane);
+}
+
+// Solve stage export: w_out[b][k] from caller covariance sums cov_in[b][k][5] (the cov_out
+// layout: sum m|y0|^2, sum m|y1|^2, Re/Im sum m y0 conj(y1), sum m).
+template <int N, bool HYB>
+__global__ void __launch_bounds__(256) avz_solve_cov_kernel(SpecArgs S, ChainArgs P) {
+  constexpr int F = N / 2 + 1;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)S.batch * F) return;
+  const int b = (int)(i / F), k = (int)(i % F);
+  double c[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) c[q] = S.cov_in[i * 5 + q];
+  const double* d = S.steer + 4 * k;
+  double w[4];
+  if constexpr (HYB) {
+    hybrid_weights_d(c, k, N, P, d[0], d[1], d[2], d[3], w);
+  } else {
+    bool sing = false;
+    mvdr_weights_d(c, k, N, P, d[0], d[1], d[2], d[3], w, &sing);
+    if (sing && P.singular_fallback == 2) atomicOr(S.flag + b, 1);
+  }
+  reinterpret_cast<float4*>(S.w_out)[i] = make_float4((float)w[0], (float)w[1], (float)w[2], (float)w[3]);
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) avz_solve_cov_fixup_kernel(SpecArgs S) {
+  constexpr int F = N / 2 + 1;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)S.batch * F) return;
+  const int b = (int)(i / F), k = (int)(i % F);
+  if (S.flag[b] == 0) return;
+  double w[4];
+  batch_fallback_weights_d(S.steer[4 * k], S.steer[4 * k + 1], w);
+  reinterpret_cast<float4*>(S.w_out)[i] = make_float4((float)w[0], (float)w[1], (float)w[2], (float)w[3]);
+}
+
+}  // namespace avz
+
+using namespace avz;
+
+template <int N, bool HYB, int PF>
+static void launch_spec_t(const SpecArgs* s, const ChainArgs* p, hipStream_t st) {
+  constexpr int F = N / 2 + 1;
+  const long long rows = (long long)s->batch * F;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  hipLaunchKernelGGL((avz_spectral_kernel<N, HYB, PF>), grid, dim3(kSpecThreads), 0, st, *s, *p);
+  if (!HYB && p->singular_fallback == 2)
+    hipLaunchKernelGGL((avz_spectral_fixup_kernel<N, PF>), grid, dim3(kSpecThreads), 0, st, *s, *p);
+}
+
+template <int N, bool HYB>
+static int launch_spec_pf(const SpecArgs* s, const ChainArgs* p, hipStream_t st) {
+  switch (p->postfilter) {
+    case PF_NONE: launch_spec_t<N, HYB, PF_NONE>(s, p, st); break;
+    case PF_EXT_FLOOR: launch_spec_t<N, HYB, PF_EXT_FLOOR>(s, p, st); break;
+    case PF_EXT_MUL: launch_spec_t<N, HYB, PF_EXT_MUL>(s, p, st); break;
+    default: return -4;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int avz_launch_spectral(int n_fft, const SpecArgs* s, const ChainArgs* p, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (s->batch <= 0) return 0;
+  if (p->singular_fallback == 2 &&
+      hipMemsetAsync(s->flag, 0, sizeof(int) * s->batch, st) != hipSuccess)
+    return -3;
+  const bool hyb = p->beamformer == BF_HYBRID_NULL;
+  if (n_fft == 1024) return hyb ? launch_spec_pf<1024, true>(s, p, st) : launch_spec_pf<1024, false>(s, p, st);
+  if (n_fft == 512) return hyb ? launch_spec_pf<512, true>(s, p, st) : launch_spec_pf<512, false>(s, p, st);
+  return -4;
+}
+
+template <int N>
+static int launch_solve_cov_t(const SpecArgs* s, const ChainArgs* p, hipStream_t st) {
+  constexpr int F = N / 2 + 1;
+  const long long n = (long long)s->batch * F;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (p->beamformer == BF_HYBRID_NULL) {
+    hipLaunchKernelGGL((avz_solve_cov_kernel<N, true>), grid, dim3(256), 0, st, *s, *p);
+  } else {
+    hipLaunchKernelGGL((avz_solve_cov_kernel<N, false>), grid, dim3(256), 0, st, *s, *p);
+    if (p->singular_fallback == 2)
+      hipLaunchKernelGGL(avz_solve_cov_fixup_kernel<N>, grid, dim3(256), 0, st, *s);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int avz_launch_solve_cov(int n_fft, const SpecArgs* s, const ChainArgs* p, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (s->batch <= 0) return 0;
+  if (p->singular_fallback == 2 &&
+      hipMemsetAsync(s->flag, 0, sizeof(int) * s->batch, st) != hipSuccess)
+    return -3;
+  if (n_fft == 1024) return launch_solve_cov_t<1024>(s, p, st);
+  if (n_fft == 512) return launch_solve_cov_t<512>(s, p, st);
+  return -4;
+}

@@ -20,6 +20,7 @@ module is injected (only TFLiteBeamformer uses it, and that class is replaced by
 _MaskFeeder below because the .tflite model file is absent).
 
 Usage:  python tests/golden/make_golden.py [hybrid] [srp] [report] [reverb] [neural] [world]
+        [spectral]
         (writes tests/golden/*.npz)
 """
 from __future__ import annotations
@@ -473,6 +474,72 @@ def gen_report(trip, metrics, save):
     save("report_test.npz", est16=est16, report=np.array(report), csv=np.array(csv_text))
 
 
+def gen_spectral(trip, save):
+    """The spectral-domain operators on STFTs of 2-s chunks of the bundled mixtures:
+    rt_av_zoom/core/tf_lite_version/inference.py batch_mvdr (:85-179) with the module's
+    own get_all_steering_vectors (:53-81) and SIGMA (:46), and its chunk driver's
+    post-filter + istft (:347-352). The module imports tensorflow at top level (absent;
+    unused by these functions): an empty stand-in is injected; its config.json is the
+    reference's own (read from the module directory). Masks are float32 like a TFLite
+    output: the chunk's oracle target mask (|S_t| >= |S_i|) and a soft one
+    (sigmoid(log|S_t| - log|S_i|)). One case zeroes bin 0 of Y at sigma = 0 so the single
+    np.linalg.solve raises LinAlgError and every bin takes the fallback (:149-153)."""
+    import importlib
+    tf = types.ModuleType("tensorflow")
+    tf.lite = types.SimpleNamespace(Interpreter=None)
+    sys.modules.setdefault("tensorflow", tf)
+    tl_dir = os.path.join(REF, "rt_av_zoom", "core", "tf_lite_version")
+    cwd = os.getcwd()
+    os.chdir(tl_dir)  # its config.json (read-only use)
+    try:
+        with contextlib.redirect_stdout(open(os.devnull, "w")):
+            tl = importlib.import_module("rt_av_zoom.core.tf_lite_version.inference")
+    finally:
+        os.chdir(cwd)
+    n_fft, hop, fs = tl.N_FFT, tl.HOP, tl.FS
+    cases = [("test_ibm", "test", 0, "ibm", tl.SIGMA), ("test_soft", "test", 0, "soft", tl.SIGMA),
+             ("set2_soft", "set2", 16000, "soft", tl.SIGMA),
+             ("test_singular", "test", 32000, "soft", 0.0)]
+    for name, k, start, kind, sigma in cases:
+        m, t, i = trip[k]
+        seg = slice(start, start + 32000)
+        chunk = (m[seg].astype(np.float64) / 32768.0).astype(np.float32)
+        f_bins, _, Y = scipy.signal.stft(chunk.T, fs=fs, nperseg=n_fft, noverlap=n_fft - hop)
+        st_ = (t[seg].astype(np.float64) / 32768.0).astype(np.float32)
+        si_ = (i[seg].astype(np.float64) / 32768.0).astype(np.float32)
+        _, _, St = scipy.signal.stft(st_, fs=fs, nperseg=n_fft, noverlap=n_fft - hop)
+        _, _, Si = scipy.signal.stft(si_, fs=fs, nperseg=n_fft, noverlap=n_fft - hop)
+        if kind == "ibm":
+            mask = (np.abs(St) >= np.abs(Si)).astype(np.float32)
+        else:
+            z = np.log(np.abs(St) + 1e-7) - np.log(np.abs(Si) + 1e-7)
+            mask = (1.0 / (1.0 + np.exp(-z))).astype(np.float32)
+        if name == "test_singular":
+            Y = Y.copy()
+            Y[:, 0, :] = 0
+        d_vecs = tl.get_all_steering_vectors(f_bins, tl.ANGLE_TARGET, tl.D, tl.C)
+        raised = []
+        o_solve = np.linalg.solve
+
+        def solve(A, b):  # records whether the reference's single solve raised
+            try:
+                return o_solve(A, b)
+            except np.linalg.LinAlgError:
+                raised.append(True)
+                raise
+        np.linalg.solve = solve
+        try:
+            S_out = tl.batch_mvdr(Y, mask, f_bins, d_vecs, sigma)
+        finally:
+            np.linalg.solve = o_solve
+        S_final = S_out * np.maximum(mask, 0.05)
+        _, chunk_out = scipy.signal.istft(S_final, fs=fs, nperseg=n_fft, noverlap=n_fft - hop)
+        save(f"spectral_{name}.npz", n_fft=n_fft, hop=hop, fs=fs, sigma=sigma, d=tl.D, c=tl.C,
+             angle=tl.ANGLE_TARGET, Y=Y.astype(np.complex64), mask=mask, f_bins=f_bins,
+             d_vectors=d_vecs[:, :, 0], S_out=S_out.astype(np.complex64),
+             chunk_out=chunk_out.astype(np.float32), fallback=bool(raised))
+
+
 def main():
     od, mm, run_metrics, metrics = install_reference()
     mpath = os.path.join(HERE, "MANIFEST.json")
@@ -502,6 +569,8 @@ def main():
             gen_neural(trip, run_metrics, save)
         if "world" in only:
             gen_world(trip, save)
+        if "spectral" in only:
+            gen_spectral(trip, save)
         with open(mpath, "w") as fh:
             json.dump(manifest, fh, indent=1, sort_keys=True)
         return
@@ -590,6 +659,7 @@ def main():
     gen_reverb(trip, run_metrics, save)
     gen_neural(trip, run_metrics, save)
     gen_world(trip, save)
+    gen_spectral(trip, save)
 
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)
