@@ -111,21 +111,21 @@ def hybrid_hard_null_bf(Y, mask, f_bins, d: float = D_FINAL) -> np.ndarray:
 
 class SpectralBeamformer:
     """Batched device form of batch_mvdr / hybrid_hard_null_bf with the chunk drivers'
-    post-filters fused (tf_lite_version/inference.py:350 S * max(M, 0.05);
+    post-filters fused (max_frames: the longest spectra istft() will see; 64 = a 2-s chunk) (tf_lite_version/inference.py:350 S * max(M, 0.05);
     Final_pipeline/src/inference.py:219 S * M) and the iSTFT of the result.
 
     kind "mvdr" (sigma 1e-5, d 0.04, floor 0.05 by default) or "hybrid" (d 0.08, x M)."""
 
     def __init__(self, kind: str = "mvdr", n_fft: int = 1024, max_items: int = 1,
                  sigma: float = SIGMA_TFLITE, d: float | None = None, floor: float | None = 0.05,
-                 max_samples: int = 32000):
+                 max_frames: int = 64):
         if kind not in ("mvdr", "hybrid"):
             raise ValueError("kind must be 'mvdr' or 'hybrid'")
         d = (D_TFLITE if kind == "mvdr" else D_FINAL) if d is None else d
         pf = "none" if floor is None else ("floor" if (kind == "mvdr" and floor > 0) else "mul")
         common = dict(n_fft=n_fft, fs=FS, mic_d=d, mask="external", postfilter=pf,
                       pf_floor=floor or 0.0, normalize="none", max_batch=max_items,
-                      max_samples=max(max_samples, n_fft))
+                      max_samples=max((max_frames - 1) * (n_fft // 2), n_fft))
         if kind == "mvdr":
             self.plan = MVDRPlan(sigma=sigma, weight_eps=1e-10, fmin_hz=0.0,
                                  singular_fallback="batch", **common)

@@ -1173,6 +1173,8 @@ static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
   const int n_items = nch * a->batch;
+  // no analysis pass in these stages: it is the analysis kernel that resets peak_u
+  if (hipMemsetAsync(a->peak_u, 0, sizeof(uint32_t) * a->batch, st) != hipSuccess) return -3;
   hipLaunchKernelGGL((avz_synthesis_kernel<N, PF, SPEC>),
                      dim3((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus())),
                      dim3(kCThreads), lds, st, *a);
