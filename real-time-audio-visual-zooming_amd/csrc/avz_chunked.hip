@@ -29,6 +29,10 @@
 
 #include "avz_common.hpp"
 
+#ifndef AVZ_BINS_V1
+#define AVZ_BINS_V1 0
+#endif
+
 namespace avz {
 
 constexpr int kChunk = 32;      // frames per chunk = bits of one mask word
@@ -116,15 +120,25 @@ __device__ __forceinline__ int utt_len(const ChainArgs& A, int b) {
   return A.len ? min(A.len[b], A.max_len) : A.max_len;
 }
 
+// IBM decision |S_int| > |S_tgt| (oracle_debug.py:49-53, strict) from the packed reference
+// pair z = tgt + i int: 2T = zr + conj(zrp), 2I = (zr - conj zrp)/i, and
+// |2T|^2 - |2I|^2 = 4 Re(zr zrp), so noise <=> Re(zr zrp) < 0 (one product, one fma).
+__device__ __forceinline__ bool ibm_noise(cf zr, cf zrp) {
+#if AVZ_BINS_V1
+  const float tr = zr.x + zrp.x, ti = zr.y - zrp.y;
+  const float ir = zr.y + zrp.y, ii = zr.x - zrp.x;
+  return ir * ir + ii * ii > tr * tr + ti * ti;
+#else
+  return fmaf(zr.x, zrp.x, -(zr.y * zrp.y)) < 0.0f;
+#endif
+}
+
 // Mask value m and covariance weight of one (bin, frame).
 template <int MASK>
 __device__ __forceinline__ float bin_mask(const ChainArgs& A, int b, cf x0, cf x1, cf zr,
                                           cf zrp, int k, int t, bool& noise, float& wgt) {
   if constexpr (MASK == MASK_IBM) {
-    // 2T = zr + conj(zrp), 2I = (zr - conj zrp)/i ; |2I|^2 > |2T|^2 <=> |I| > |T|
-    const float tr = zr.x + zrp.x, ti = zr.y - zrp.y;
-    const float ir = zr.y + zrp.y, ii = zr.x - zrp.x;
-    noise = ir * ir + ii * ii > tr * tr + ti * ti;
+    noise = ibm_noise(zr, zrp);
     wgt = noise ? 1.0f : 0.0f;
     return wgt;
   } else if constexpr (MASK == MASK_IPD) {
@@ -216,10 +230,12 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
 
   Acc32 acc[BPT];
   uint32_t bits[BPT];
+  int ipd_clear_n[BPT];  // IPD: frames the cross-product test weighted 1
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
     acc[j].zero();
     bits[j] = 0u;
+    ipd_clear_n[j] = 0;
   }
   // IRM post-filter gains of this chunk (PF_IRM plans only)
   static_assert(!IRM || MASK == MASK_IBM, "IRM needs the references");
@@ -303,11 +319,24 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
               if constexpr (MASK == MASK_IPD) {
                 // the exact angle test of near-colinear bins runs after the loop
                 const bool clear = ipd_clear(x0, x1);
-                const float w = clear ? 1.0f : 0.0f;
                 ipd_fix[j] |= (clear ? 0u : 1u) << (g0 + i);
+#if AVZ_BINS_V1
+                const float w = clear ? 1.0f : 0.0f;
                 acc[j].add(x0, x1, w, w);
+#else
+                acc[j].add_sel(x0, x1, clear);  // weight count: nclear below
+#endif
                 continue;
               }
+#if !AVZ_BINS_V1
+              if constexpr (MASK == MASK_IBM) {
+                const bool noise = ibm_noise(zr[i], zrp[i]);
+                bits[j] |= (noise ? 1u : 0u) << (step * FB + g0 + i);
+                acc[j].add_sel(x0, x1, noise);  // weight count: popcount of bits at the end
+                if constexpr (IRM) gain[(step * FB + g0 + i) * F + kb] = irm_gain(zr[i], zrp[i]);
+                continue;
+              }
+#endif
               bool noise = false;
               float wgt;
               float m;
@@ -345,6 +374,9 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         const int kb = tid + j * NT;
         const int kp = (N - kb) & (N - 1);
         uint32_t f = ipd_fix[j];
+#if !AVZ_BINS_V1
+        ipd_clear_n[j] += nvalid - __popc(f);  // frames weighted 1 by add_sel
+#endif
         while (f) {
           const int i = __builtin_ctz(f);
           f &= f - 1u;
@@ -382,6 +414,11 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
     const int kb = tid + j * NT;
+#if !AVZ_BINS_V1
+    // binary weights were folded into the selects: their count is exact in fp32
+    if constexpr (MASK == MASK_IBM) acc[j].cm = (float)__popc(bits[j]);
+    if constexpr (MASK == MASK_IPD) acc[j].cm += (float)ipd_clear_n[j];
+#endif
     P[0 * F + kb] = acc[j].c00;
     P[1 * F + kb] = acc[j].c11;
     P[2 * F + kb] = acc[j].c01r;

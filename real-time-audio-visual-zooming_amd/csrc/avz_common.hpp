@@ -219,6 +219,20 @@ struct Acc32 {
     c01i = fmaf(wgt, x0.y * x1.x - x0.x * x1.y, c01i);  // Im x0 conj(x1)
     cm += m;
   }
+  // Binary weight (IBM, clear IPD frames): the selected inputs carry the weight (w^2 = w),
+  // 4 selects + 8 fma; the weight count goes to cm separately (popcount of the bits).
+  __device__ __forceinline__ void add_sel(cf x0, cf x1, bool on) {
+    const cf m0 = on ? x0 : cf{0.f, 0.f};
+    const cf m1 = on ? x1 : cf{0.f, 0.f};
+    c00 = fmaf(m0.x, x0.x, c00);
+    c00 = fmaf(m0.y, x0.y, c00);
+    c11 = fmaf(m1.x, x1.x, c11);
+    c11 = fmaf(m1.y, x1.y, c11);
+    c01r = fmaf(m0.x, x1.x, c01r);  // Re x0 conj(x1)
+    c01r = fmaf(m0.y, x1.y, c01r);
+    c01i = fmaf(m0.y, x1.x, c01i);  // Im x0 conj(x1)
+    c01i = fmaf(-m0.x, x1.y, c01i);
+  }
 };
 struct Acc64 {
   double c[5];
