@@ -71,6 +71,9 @@ def parse():
                     help="STFT size (hop n/2); 1024 is the BASELINE configs, 512 oracle_debug's default")
     ap.add_argument("--unet-dtype", choices=("fp32", "bf16"), default="fp32",
                     help="unet workload: U-Net forward precision (fp32 = the reference's)")
+    ap.add_argument("--scenes", choices=("philox", "host"), default="philox",
+                    help="input scenes: generated on the device (avz_scene_generate) or the "
+                         "host numpy generator (make_batch)")
     ap.add_argument("--rehearse-shared-gpu", action="store_true",
                     help="N > 1 rehearsal on one GPU: all ranks on cuda:0, gloo collectives")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -139,8 +142,8 @@ def cpu_baseline(sample, seconds, workers, workload):
 
 
 # ----------------------------------------------------------------------------- workloads
-def setup_chain(args, B, S, dev, mix, tgt, itf):
-    """ibm / ipd: one avz_mvdr_batch call per step."""
+def setup_chain(args, B, S, dev, d_mix, d_tgt, d_itf):
+    """ibm / ipd: one avz_mvdr_batch call per step (inputs already resident in HBM)."""
     import torch
 
     import avz
@@ -152,10 +155,9 @@ def setup_chain(args, B, S, dev, mix, tgt, itf):
         plan = avz.MVDRPlan(n_fft=N_FFT, sigma=1e-7, mic_d=0.01, mask="ipd", postfilter="none",
                             normalize="peak", norm_eps=1e-6, max_batch=B, max_samples=S)
         streams = 2
-    d_mix = torch.from_numpy(mix).to(dev)
     refs = {}
     if args.workload == "ibm":
-        refs = dict(ref_tgt=torch.from_numpy(tgt).to(dev), ref_int=torch.from_numpy(itf).to(dev))
+        refs = dict(ref_tgt=d_tgt, ref_int=d_itf)
     lens = torch.full((B,), S, dtype=torch.int32, device=dev)
     out = plan.alloc_out(B, S, dev)
     peak = torch.empty((B,), dtype=torch.float32, device=dev)
@@ -168,11 +170,11 @@ def setup_chain(args, B, S, dev, mix, tgt, itf):
     info = dict(plan=plan, out=out[:, :min(n_out, S)], bins=B * F * T,
                 alg_analysis=B * streams * S * 4, alg_chain=B * (streams * S * 4 + n_out * 4),
                 kernel=f"avz_analysis_kernel<{N_FFT},{'IBM' if args.workload == 'ibm' else 'IPD'}>",
-                mix=d_mix, refs=refs, host=(mix, tgt, itf))
+                mix=d_mix, refs=refs)
     return step, info
 
 
-def setup_unet(args, B, S, dev, mix):
+def setup_unet(args, B, S, dev, d_mix):
     import torch
 
     from avz import neural as N
@@ -181,7 +183,6 @@ def setup_unet(args, B, S, dev, mix):
     n_items = B * -(-S // 16000)
     dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[args.unet_dtype]
     bf = N.NeuralMaskBeamformer(model, max_items=n_items, model_dtype=dt)
-    d_mix = torch.from_numpy(mix).to(dev)
     y = {}
 
     def step():
@@ -210,14 +211,15 @@ def main():
     B = args.batch
 
     from avz import synth
-    mix, tgt, itf = synth.make_batch(B, start=rank * B, n_samples=S,
-                                     n_interferers=args.interferers)
+    gen_host = synth.make_batch_philox if args.scenes == "philox" else synth.make_batch
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.workload != "unet":
         workers = args.cpu_workers or min(16, len(os.sched_getaffinity(0)))
         k = min(B, 32)
-        cpu = cpu_baseline((mix[:k], tgt[:k], itf[:k]), args.cpu_seconds, workers, args.workload)
+        # the host restatement of the same scenes (forked before any GPU initialisation)
+        sample = gen_host(k, start=rank * B, n_samples=S, n_interferers=args.interferers)
+        cpu = cpu_baseline(sample, args.cpu_seconds, workers, args.workload)
 
     import torch
     import torch.distributed as dist
@@ -236,10 +238,23 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
 
-    if args.workload == "unet":
-        step, info = setup_unet(args, B, S, dev, mix)
+    # this rank's shard of utterances rank * B .. rank * B + B - 1, generated in HBM
+    g0 = time.perf_counter()
+    if args.scenes == "philox":
+        d_mix, d_tgt, d_itf = synth.make_batch_device(B, start=rank * B, n_samples=S,
+                                                      n_interferers=args.interferers,
+                                                      device=dev, rng="philox")
     else:
-        step, info = setup_chain(args, B, S, dev, mix, tgt, itf)
+        hm, ht, hi = synth.make_batch(B, start=rank * B, n_samples=S,
+                                      n_interferers=args.interferers)
+        d_mix, d_tgt, d_itf = (torch.from_numpy(a).to(dev) for a in (hm, ht, hi))
+    torch.cuda.synchronize()
+    gen_ms = 1e3 * (time.perf_counter() - g0)
+
+    if args.workload == "unet":
+        step, info = setup_unet(args, B, S, dev, d_mix)
+    else:
+        step, info = setup_chain(args, B, S, dev, d_mix, d_tgt, d_itf)
     plan = info["plan"]
 
     for _ in range(args.warmup):
@@ -297,12 +312,12 @@ def main():
             # PCIe-inclusive rate (not `value`): the same step with its inputs copied from
             # pinned host memory first and the output copied back (host-buffer callers, e.g.
             # the oracle_debug.main mirror). Reported beside the HBM-resident number.
-            pin = lambda x: torch.from_numpy(x).pin_memory()  # noqa: E731
+            pin = lambda x: x.cpu().pin_memory()  # noqa: E731
             ho = torch.empty(tuple(info["out"].shape), dtype=torch.float32).pin_memory()
-            d_in = [(pin(info["host"][0]), info["mix"])]
+            d_in = [(pin(info["mix"]), info["mix"])]
             if info["refs"]:
-                d_in += [(pin(info["host"][1]), info["refs"]["ref_tgt"]),
-                         (pin(info["host"][2]), info["refs"]["ref_int"])]
+                d_in += [(pin(info["refs"]["ref_tgt"]), info["refs"]["ref_tgt"]),
+                         (pin(info["refs"]["ref_int"]), info["refs"]["ref_int"])]
             n_pcie = max(2, K // 4)
             torch.cuda.synchronize()
             p0 = time.perf_counter()
@@ -328,9 +343,7 @@ def main():
     else:
         est_out = info["out"][:, :L]
         L = est_out.shape[1]
-    d_mix = info["mix"]
-    d_tgt = torch.from_numpy(tgt[:, :L]).to(dev)
-    d_itf = torch.from_numpy(itf[:, :L]).to(dev)
+    d_tgt, d_itf = d_tgt[:, :L], d_itf[:, :L]
     est = torch.cat([est_out, d_mix[:, 0, :L]])
     m = metrics.projection_metrics(est, torch.cat([d_tgt] * 2), torch.cat([d_itf] * 2))
     sir_out, sir_in = m[:B, 3], m[B:, 3]
@@ -351,6 +364,7 @@ def main():
     if rank == 0 and args.workload != "unet":
         k = min(B, 4)
         got = sir_out[:k].cpu().numpy()
+        mix, tgt, itf = (x[:k].cpu().numpy() for x in (d_mix, d_tgt, d_itf))
         refs = []
         for b in range(k):
             if args.workload == "ipd":
@@ -423,7 +437,11 @@ def main():
             "metric": METRIC, "value": value, "unit": "TF-bins/s", "n_gpus": world,
             "steps": K, "warmup": args.warmup, "ms_per_step": 1e3 * t_max / K,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic speech-like 2-mic far-field mixtures (SURVEY 8(d)), seeds 1000+idx",
+            "data": ("synthetic speech-like 2-mic far-field mixtures (SURVEY 8(d) model), "
+                     + ("generated in HBM by avz_scene_generate (Philox draws keyed by utterance "
+                        f"index rank*B+b; {gen_ms:.1f} ms for this rank's shard)"
+                        if args.scenes == "philox" else
+                        f"host numpy generator, seeds 1000+idx ({gen_ms:.0f} ms incl. H2D)")),
             "config": cfg,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -290,13 +290,30 @@ int avz_projection_metrics(int batch, int max_len, const int* len, const float* 
  * angles_deg[b][s]; noise[b][c][0..n) unit-normal draws for mic c. Writes
  * mix[b][c] (at mix_stride / ch_stride), tgt[b] = mic-1 target image / peak,
  * itf[b] = mic-1 interference image / peak. `workspace` holds
- * avz_scene_workspace_bytes(batch, n_src, n) bytes. All arrays device-resident. */
+ * avz_scene_workspace_bytes(batch, n_src, n) bytes. All arrays device-resident.
+ * n even. When n factors into 2, 3 and 5 the delays run as fp64 mixed-radix FFTs
+ * (O(n log n)); otherwise as the exact O(n^2) circular convolution. */
 long long avz_scene_workspace_bytes(int batch, int n_src, int n);
 int avz_scene_mix(int batch, int n_src, int n, const float* src, const double* angles_deg,
                   const float* noise, double mic_d, double c_sound, double fs, double sir_db,
                   double snr_db, float* mix, long long mix_stride, long long ch_stride,
                   float* tgt, float* itf, long long ref_stride, void* workspace,
                   long long workspace_bytes, void* hip_stream);
+
+/* The whole scene on the device (the sharded batch driver's input path): utterance
+ * start_idx + b draws from counter-based Philox4x32-10 streams keyed by (start_idx + b,
+ * 0x5CE7E5ED ^ seed) — Box-Muller normals for the speech-like sources (AR(2) poles 0.9 /
+ * 0.5, |sin(2 pi 4 t + phi)| envelope, 25 % of 250-ms blocks silenced: synth.speech_like)
+ * and the AWGN, uniforms for the envelope phases, the kept blocks and the azimuths of
+ * interferers 2.. (target 90 deg, interferer 1 at 40 deg) — then avz_scene_mix's model.
+ * avz/synth.py make_scene_philox is the host restatement. `workspace` holds
+ * avz_scene_generate_workspace_bytes(batch, n_interferers, n) bytes. */
+long long avz_scene_generate_workspace_bytes(int batch, int n_interferers, int n);
+int avz_scene_generate(int batch, long long start_idx, int n_interferers, int n, unsigned seed,
+                       double mic_d, double c_sound, double fs, double sir_db, double snr_db,
+                       float* mix, long long mix_stride, long long ch_stride, float* tgt,
+                       float* itf, long long ref_stride, void* workspace,
+                       long long workspace_bytes, void* hip_stream);
 
 const char* avz_strerror(int code);
 /* Last HIP error string recorded by the library on this thread (diagnostics). */

@@ -38,7 +38,7 @@ EXPORTED = [
     "avz_projection_metrics", "avz_scene_workspace_bytes", "avz_scene_mix", "avz_strerror",
     "avz_last_hip_error", "avz_version", "avz_mvdr_workspace_bytes",
     "avz_mvdr_covariance", "avz_solve_covariance", "avz_apply_istft", "avz_beamform_spectral",
-    "avz_istft",
+    "avz_istft", "avz_scene_generate_workspace_bytes", "avz_scene_generate",
 ]
 
 
@@ -138,6 +138,10 @@ def _load():
     lib.avz_scene_workspace_bytes.argtypes = [I, I, I]
     lib.avz_scene_workspace_bytes.restype = LL
     lib.avz_scene_mix.argtypes = [I, I, I, P, P, P, D, D, D, D, D, P, LL, LL, P, P, LL, P, LL, P]
+    lib.avz_scene_generate_workspace_bytes.argtypes = [I, I, I]
+    lib.avz_scene_generate_workspace_bytes.restype = LL
+    lib.avz_scene_generate.argtypes = [I, LL, I, I, ct.c_uint, D, D, D, D, D, P, LL, LL, P, P, LL,
+                                       P, LL, P]
     lib.avz_strerror.argtypes = [ct.c_int]
     lib.avz_strerror.restype = ct.c_char_p
     lib.avz_last_hip_error.restype = ct.c_char_p
@@ -145,7 +149,7 @@ def _load():
                  "avz_mvdr_batch", "avz_stft", "avz_chunk_split", "avz_chunk_merge",
                  "avz_plan_set_timing", "avz_plan_get_timing", "avz_mask_features",
                  "avz_srp_scan", "avz_projection_metrics", "avz_scene_mix",
-                 "avz_version"):
+                 "avz_scene_generate", "avz_version"):
         getattr(lib, name).restype = ct.c_int
     return lib
 

@@ -3,9 +3,12 @@
 The reference loops serially over run names (sim -> inf -> eval -> CSV row, exceptions
 swallowed per item). Here the utterance batch is the unit of work: utterances
 [start, start + n) are split contiguously over the ranks of a torch.distributed group
-(one process per GPU), each rank generates its scenes, runs ONE fused MVDR launch per
-chunk of ``batch`` utterances, scores them on the device, and the only collective is
-an all-reduce of the metric sums (RCCL over xGMI on GPUs, gloo in CPU tests).
+(one process per GPU), each rank generates its scenes ON THE DEVICE (avz_scene_generate:
+counter-based draws, FFT fractional delays — milliseconds for a 512-utterance shard, so
+the host never feeds the GPU), runs ONE fused MVDR launch per chunk of ``batch``
+utterances, scores them on the device, and the only collective is an all-reduce of the
+metric sums (RCCL over xGMI on GPUs, gloo in CPU tests; on a CPU device the scenes come
+from the generator's host restatement, synth.make_batch_philox, so they are the same).
 
 Rows follow batch_metrics.csv (Final_pipeline/src/metrics.py:16-44); STOI/PESQ are
 reported as 0.0, exactly what the reference writes when pystoi/pesq are missing
@@ -67,8 +70,10 @@ def gpu_enhancer(n_fft=1024, sigma=1.0, mic_d=0.01, max_batch=256, max_samples=6
 
 def run_batch(n_runs: int, start_idx: int = 0, n_interferers: int = 2, *,
               seconds: float = 4.0, batch: int = 256, device=None,
-              enhance: Callable | None = None, csv_path: str | None = None) -> BatchResult:
-    """batch_run.run_batch equivalent over a device batch, sharded over the group."""
+              enhance: Callable | None = None, csv_path: str | None = None,
+              scenes: str = "philox") -> BatchResult:
+    """batch_run.run_batch equivalent over a device batch, sharded over the group.
+    scenes: "philox" (device generator; host restatement on CPU) or "host" (make_batch)."""
     rank, world = world_info()
     lo, hi = shard(n_runs, rank, world)
     dev = torch.device(device) if device is not None else (
@@ -81,10 +86,16 @@ def run_batch(n_runs: int, start_idx: int = 0, n_interferers: int = 2, *,
     sums = torch.zeros(5, dtype=torch.float64, device=dev)
     for c0 in range(start_idx + lo, start_idx + hi, batch):
         nb = min(batch, start_idx + hi - c0)
-        mix, tgt, itf = synth.make_batch(nb, start=c0, n_samples=S, n_interferers=n_interferers)
-        d_mix = torch.from_numpy(mix).to(dev)
-        d_tgt = torch.from_numpy(tgt).to(dev)
-        d_itf = torch.from_numpy(itf).to(dev)
+        if scenes == "philox" and dev.type == "cuda":
+            d_mix, d_tgt, d_itf = synth.make_batch_device(nb, start=c0, n_samples=S,
+                                                          n_interferers=n_interferers,
+                                                          device=dev, rng="philox")
+        else:
+            gen = synth.make_batch_philox if scenes == "philox" else synth.make_batch
+            mix, tgt, itf = gen(nb, start=c0, n_samples=S, n_interferers=n_interferers)
+            d_mix = torch.from_numpy(mix).to(dev)
+            d_tgt = torch.from_numpy(tgt).to(dev)
+            d_itf = torch.from_numpy(itf).to(dev)
         out = enhance(d_mix, d_tgt, d_itf)
         L = min(out.shape[-1], S)
         osinr_b, osir_b = metrics.calculate_osnr_osir(d_mix[:, 0, :L], d_tgt[:, :L], d_itf[:, :L])

@@ -161,12 +161,140 @@ def scene_draws(idx: int, n_samples: int = 64000, n_interferers: int = 1, fs: in
     return np.array([90.0] + angles[:n_interferers]), np.stack(srcs), z
 
 
+# ---------------------------------------------------------------- counter-based draws
+# The device generator (avz_scene_generate, csrc/avz_scene.hip) draws from Philox4x32-10
+# streams keyed by (utterance index, SCENE_KEY ^ seed); this is its host restatement.
+SCENE_KEY = 0x5CE7E5ED
+STREAM_NOISE, STREAM_UNIF = 0x100, 0x200
+UNIF_PHASE, UNIF_KEEP = 0x1000, 0x100000
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32(c0, c1, c2, c3, k0: int, k1: int):
+    """Random123 philox4x32-10 on uint32 counter arrays; returns four uint64 arrays < 2^32."""
+    c0, c1, c2, c3 = (np.asarray(c, np.uint64) & _M32 for c in (c0, c1, c2, c3))
+    k0, k1 = np.uint64(k0 & 0xFFFFFFFF), np.uint64(k1 & 0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c0
+        p1 = np.uint64(0xCD9E8D57) * c2
+        c0, c1, c2, c3 = (p1 >> np.uint64(32)) ^ c1 ^ k0, p1 & _M32, (p0 >> np.uint64(32)) ^ c3 ^ k1, p0 & _M32
+        k0 = (k0 + np.uint64(0x9E3779B9)) & _M32
+        k1 = (k1 + np.uint64(0xBB67AE85)) & _M32
+    return c0, c1, c2, c3
+
+
+def _u53(hi, lo):
+    return (((hi << np.uint64(32)) | lo) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+
+
+def _key(idx: int, seed: int = 0):
+    return idx & 0xFFFFFFFF, ((idx >> 32) ^ SCENE_KEY ^ seed) & 0xFFFFFFFF
+
+
+def philox_normals(key, stream: int, n: int) -> np.ndarray:
+    """n standard normals of a stream: pair i = Box-Muller of block i's two 53-bit uniforms."""
+    i = np.arange((n + 1) // 2, dtype=np.uint64)
+    x, y, z, w = philox4x32(i, stream, 0, 0, *key)
+    u1 = (((x << np.uint64(32)) | y) >> np.uint64(11)).astype(np.float64)
+    u1 = (u1 + 1.0) * 2.0 ** -53
+    u2 = _u53(z, w)
+    r = np.sqrt(-2.0 * np.log(u1))
+    out = np.empty(2 * len(i))
+    out[0::2] = r * np.cos(2.0 * np.pi * u2)
+    out[1::2] = r * np.sin(2.0 * np.pi * u2)
+    return out[:n]
+
+
+def philox_uniform(key, j) -> np.ndarray:
+    x, y, _, _ = philox4x32(np.asarray(j, np.uint64), STREAM_UNIF, 0, 0, *key)
+    return _u53(x, y)
+
+
+def speech_like_philox(key, s: int, n: int, fs: int = FS) -> np.ndarray:
+    """speech_like() on the counter-based streams of source s."""
+    y = lfilter([1.0], [1.0, -1.4, 0.45], philox_normals(key, s, n))
+    phi = np.pi * philox_uniform(key, UNIF_PHASE + s)
+    t = np.arange(n) / fs
+    env = np.abs(np.sin(2 * np.pi * 4.0 * t + phi))
+    blk = int(0.25 * fs)
+    nb = -(-n // blk)
+    keep = philox_uniform(key, UNIF_KEEP * (1 + s) + np.arange(nb)) >= 0.25
+    env *= np.repeat(keep, blk)[:n]
+    return y * env
+
+
+def scene_draws_philox(idx: int, n_samples: int = 64000, n_interferers: int = 1,
+                       fs: int = FS, seed: int = 0):
+    """(angles [1 + K], sources [1 + K, S], unit-normal noise [2, S]) of utterance idx."""
+    key = _key(idx, seed)
+    K = n_interferers
+    angles = [90.0] + ([40.0] if K >= 1 else [])
+    if K > 1:
+        angles += list(180.0 * philox_uniform(key, np.arange(K - 1)))
+    srcs = np.stack([speech_like_philox(key, s, n_samples, fs) for s in range(1 + K)])
+    z = np.stack([philox_normals(key, STREAM_NOISE + c, n_samples) for c in range(2)])
+    return np.array(angles), srcs, z
+
+
+def mix_draws(angles, srcs, z, d: float = MIC_D, sir_db: float = 0.0, snr_db: float = 5.0,
+              fs: int = FS):
+    """make_scene's mixing (delays, SIR gain on mic 1, AWGN, shared peak) of given draws."""
+    n = srcs.shape[-1]
+    K = len(angles) - 1
+    t1, t2 = far_field_delays(angles[0], d)
+    tgt_m = [frac_delay(srcs[0], t1, fs), frac_delay(srcs[0], t2, fs)]
+    int_m = [np.zeros(n), np.zeros(n)]
+    for k in range(1, K + 1):
+        d1, d2 = far_field_delays(angles[k], d)
+        int_m[0] += frac_delay(srcs[k], d1, fs)
+        int_m[1] += frac_delay(srcs[k], d2, fs)
+    p_t, p_i = np.mean(tgt_m[0] ** 2), np.mean(int_m[0] ** 2)
+    if K > 0 and p_i > 0:
+        g = np.sqrt(p_t / (p_i * 10 ** (sir_db / 10)))
+        int_m = [g * int_m[0], g * int_m[1]]
+    mix = []
+    for c in range(2):
+        cl = tgt_m[c] + int_m[c]
+        p = np.mean(cl ** 2)
+        mix.append(cl if p == 0 else cl + np.sqrt(p / (10 ** (snr_db / 10))) * z[c])
+    mix = np.stack(mix)
+    peak = np.max(np.abs(mix)) + 1e-9
+    return ((mix / peak).astype(np.float32), (tgt_m[0] / peak).astype(np.float32),
+            (int_m[0] / peak).astype(np.float32))
+
+
+def make_scene_philox(idx: int, n_samples: int = 64000, n_interferers: int = 1,
+                      d: float = MIC_D, sir_db: float = 0.0, snr_db: float = 5.0,
+                      fs: int = FS, seed: int = 0):
+    """Host restatement of avz_scene_generate for one utterance (make_scene's model on the
+    counter-based draws)."""
+    a, s, z = scene_draws_philox(idx, n_samples, n_interferers, fs, seed)
+    return mix_draws(a, s, z, d, sir_db, snr_db, fs)
+
+
+def make_batch_philox(batch: int, start: int = 0, n_samples: int = 64000,
+                      n_interferers: int = 2, seed: int = 0, **kw):
+    mix = np.empty((batch, 2, n_samples), np.float32)
+    tgt = np.empty((batch, n_samples), np.float32)
+    itf = np.empty((batch, n_samples), np.float32)
+    for b in range(batch):
+        mix[b], tgt[b], itf[b] = make_scene_philox(start + b, n_samples, n_interferers,
+                                                   seed=seed, **kw)
+    return mix, tgt, itf
+
+
 def make_batch_device(batch: int, start: int = 0, n_samples: int = 64000,
                       n_interferers: int = 2, d: float = MIC_D, sir_db: float = 0.0,
-                      snr_db: float = 5.0, fs: int = FS, device=None):
-    """make_batch on the device: the host draws the sources and noise (same RNG stream
-    as make_scene), avz_scene_mix does the fractional delays, SIR gain, AWGN and peak
-    normalisation. Returns device tensors (mix [B, 2, S], tgt [B, S], itf [B, S])."""
+                      snr_db: float = 5.0, fs: int = FS, device=None, rng: str = "host",
+                      seed: int = 0):
+    """A batch of scenes as device tensors (mix [B, 2, S], tgt [B, S], itf [B, S]).
+
+    rng="host":   make_batch's scenes — the host draws the sources and noise (same RNG
+                  stream as make_scene) and avz_scene_mix does the delays, SIR gain, AWGN
+                  and peak normalisation.
+    rng="philox": avz_scene_generate — draws and all on the device (make_batch_philox is
+                  the host restatement); no host work, so a large shard costs milliseconds.
+    """
     import ctypes as ct
 
     import torch
@@ -175,6 +303,20 @@ def make_batch_device(batch: int, start: int = 0, n_samples: int = 64000,
     from .engine import _stream_handle
     dev = device or torch.device("cuda", torch.cuda.current_device())
     K = n_interferers
+    mix = torch.empty((batch, 2, n_samples), dtype=torch.float32, device=dev)
+    tgt = torch.empty((batch, n_samples), dtype=torch.float32, device=dev)
+    itf = torch.empty((batch, n_samples), dtype=torch.float32, device=dev)
+    p = lambda t: ct.c_void_p(t.data_ptr())  # noqa: E731
+    if rng == "philox":
+        ws_bytes = lib.avz_scene_generate_workspace_bytes(batch, K, n_samples)
+        ws = torch.empty((max(ws_bytes, 4) + 3) // 4, dtype=torch.float32, device=dev)
+        check(lib.avz_scene_generate(batch, start, K, n_samples, seed, d, C_SOUND, float(fs),
+                                     sir_db, snr_db, p(mix), mix.stride(0), mix.stride(1), p(tgt),
+                                     p(itf), tgt.stride(0), p(ws), ws_bytes,
+                                     _stream_handle(None)), "avz_scene_generate")
+        return mix, tgt, itf
+    if rng != "host":
+        raise ValueError(f"rng must be 'host' or 'philox', not {rng!r}")
     angles = np.empty((batch, 1 + K))
     srcs = np.empty((batch, 1 + K, n_samples), np.float32)
     noise = np.empty((batch, 2, n_samples), np.float32)
@@ -183,12 +325,8 @@ def make_batch_device(batch: int, start: int = 0, n_samples: int = 64000,
     d_ang = torch.from_numpy(angles).to(dev)
     d_src = torch.from_numpy(srcs).to(dev)
     d_noise = torch.from_numpy(noise).to(dev)
-    mix = torch.empty((batch, 2, n_samples), dtype=torch.float32, device=dev)
-    tgt = torch.empty((batch, n_samples), dtype=torch.float32, device=dev)
-    itf = torch.empty((batch, n_samples), dtype=torch.float32, device=dev)
     ws_bytes = lib.avz_scene_workspace_bytes(batch, 1 + K, n_samples)
     ws = torch.empty((max(ws_bytes, 4) + 3) // 4, dtype=torch.float32, device=dev)
-    p = lambda t: ct.c_void_p(t.data_ptr())  # noqa: E731
     check(lib.avz_scene_mix(batch, 1 + K, n_samples, p(d_src), p(d_ang), p(d_noise), d, C_SOUND,
                             float(fs), sir_db, snr_db, p(mix), mix.stride(0), mix.stride(1),
                             p(tgt), p(itf), tgt.stride(0), p(ws), ws_bytes,

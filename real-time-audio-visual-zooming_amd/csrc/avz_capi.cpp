@@ -646,7 +646,42 @@ extern "C" int avz_srp_scan(const avz_plan* p, int batch, const int* len, int ma
 
 extern "C" long long avz_scene_workspace_bytes(int batch, int n_src, int n) {
   if (batch <= 0 || n_src <= 0 || n <= 0) return 0;
-  return 2LL * batch * n_src * 2 * n * (long long)sizeof(float);
+  return avz_scene_mix_ws(batch, n_src, n);
+}
+
+static int scene_check(int batch, int n_src, int n, double fs, double c_sound, float* mix,
+                       long long mix_stride, long long ch_stride, float* tgt, float* itf,
+                       long long ref_stride, void* workspace) {
+  if (batch < 0 || n_src < 1 || n < 2 || (n & 1)) return AVZ_ERR_SHAPE;  // irfft pairs: n even
+  if (batch == 0) return AVZ_OK;
+  if (!mix || !tgt || !itf || !workspace) return AVZ_ERR_ARG;
+  if (!(fs > 0) || !(c_sound > 0)) return AVZ_ERR_ARG;
+  if (ch_stride < n || (batch > 1 && (mix_stride < ch_stride + n || ref_stride < n)))
+    return AVZ_ERR_SHAPE;
+  if (batch > 65535) return AVZ_ERR_UNSUPPORTED;  // grid.y
+  return AVZ_OK;
+}
+
+static avz::SceneArgs scene_args(int batch, int n_src, int n, double mic_d, double c_sound,
+                                 double fs, double sir_db, double snr_db, float* mix,
+                                 long long mix_stride, long long ch_stride, float* tgt,
+                                 float* itf, long long ref_stride) {
+  avz::SceneArgs s{};
+  s.batch = batch;
+  s.n_src = n_src;
+  s.n = n;
+  s.mic_d = mic_d;
+  s.c_sound = c_sound;
+  s.fs = fs;
+  s.sir_db = sir_db;
+  s.snr_db = snr_db;
+  s.mix = mix;
+  s.mix_stride = mix_stride;
+  s.ch_stride = ch_stride;
+  s.tgt = tgt;
+  s.itf = itf;
+  s.ref_stride = ref_stride;
+  return s;
 }
 
 extern "C" int avz_scene_mix(int batch, int n_src, int n, const float* src,
@@ -655,36 +690,46 @@ extern "C" int avz_scene_mix(int batch, int n_src, int n, const float* src,
                              long long mix_stride, long long ch_stride, float* tgt, float* itf,
                              long long ref_stride, void* workspace, long long workspace_bytes,
                              void* stream) {
-  if (batch < 0 || n_src < 1 || n < 2 || (n & 1)) return AVZ_ERR_SHAPE;  // irfft pairs: n even
-  if (batch == 0) return AVZ_OK;
-  if (!src || !angles_deg || !noise || !mix || !tgt || !itf || !workspace) return AVZ_ERR_ARG;
-  if (!(fs > 0) || !(c_sound > 0)) return AVZ_ERR_ARG;
-  if (ch_stride < n || (batch > 1 && (mix_stride < ch_stride + n || ref_stride < n)))
-    return AVZ_ERR_SHAPE;
+  const int rc0 = scene_check(batch, n_src, n, fs, c_sound, mix, mix_stride, ch_stride, tgt, itf,
+                              ref_stride, workspace);
+  if (rc0 != AVZ_OK || batch == 0) return rc0;
+  if (!src || !angles_deg || !noise) return AVZ_ERR_ARG;
   if (workspace_bytes < avz_scene_workspace_bytes(batch, n_src, n)) return AVZ_ERR_SHAPE;
-  if ((long long)batch * n_src * 2 > 65535) return AVZ_ERR_UNSUPPORTED;  // grid.y
-  avz::SceneArgs s{};
-  s.batch = batch;
-  s.n_src = n_src;
-  s.n = n;
+  if (!avz_scene_fft_len(n) && (long long)batch * n_src * 2 > 65535)  // O(n^2) path grid.y
+    return AVZ_ERR_UNSUPPORTED;
+  avz::SceneArgs s = scene_args(batch, n_src, n, mic_d, c_sound, fs, sir_db, snr_db, mix,
+                                mix_stride, ch_stride, tgt, itf, ref_stride);
   s.src = src;
   s.angles_deg = angles_deg;
   s.noise = noise;
-  s.mic_d = mic_d;
-  s.c_sound = c_sound;
-  s.fs = fs;
-  s.sir_db = sir_db;
-  s.snr_db = snr_db;
-  const long long per = (long long)batch * n_src * 2 * n;
-  s.hk = static_cast<float*>(workspace);
-  s.img = s.hk + per;
-  s.mix = mix;
-  s.mix_stride = mix_stride;
-  s.ch_stride = ch_stride;
-  s.tgt = tgt;
-  s.itf = itf;
-  s.ref_stride = ref_stride;
-  const int rc = avz_launch_scene(&s, stream);
+  const int rc = avz_launch_scene(&s, workspace, stream);
+  if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
+  return rc;
+}
+
+extern "C" long long avz_scene_generate_workspace_bytes(int batch, int n_interferers, int n) {
+  if (batch <= 0 || n_interferers < 0 || n <= 0) return 0;
+  return avz_scene_gen_ws(batch, 1 + n_interferers, n);
+}
+
+extern "C" int avz_scene_generate(int batch, long long start_idx, int n_interferers, int n,
+                                  unsigned seed, double mic_d, double c_sound, double fs,
+                                  double sir_db, double snr_db, float* mix, long long mix_stride,
+                                  long long ch_stride, float* tgt, float* itf,
+                                  long long ref_stride, void* workspace,
+                                  long long workspace_bytes, void* stream) {
+  if (n_interferers < 0 || start_idx < 0) return AVZ_ERR_ARG;
+  const int n_src = 1 + n_interferers;
+  const int rc0 = scene_check(batch, n_src, n, fs, c_sound, mix, mix_stride, ch_stride, tgt, itf,
+                              ref_stride, workspace);
+  if (rc0 != AVZ_OK || batch == 0) return rc0;
+  if (workspace_bytes < avz_scene_generate_workspace_bytes(batch, n_interferers, n))
+    return AVZ_ERR_SHAPE;
+  if (!avz_scene_fft_len(n) && (long long)batch * n_src * 2 > 65535)  // O(n^2) path grid.y
+    return AVZ_ERR_UNSUPPORTED;
+  avz::SceneArgs s = scene_args(batch, n_src, n, mic_d, c_sound, fs, sir_db, snr_db, mix,
+                                mix_stride, ch_stride, tgt, itf, ref_stride);
+  const int rc = avz_launch_scene_generate(&s, start_idx, seed, workspace, stream);
   if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
   return rc;
 }

@@ -139,8 +139,8 @@ struct SceneArgs {
   const double* angles_deg;   // [B][n_src] azimuths
   const float* noise;         // [B][2][n] unit-normal AWGN draws
   double mic_d, c_sound, fs, sir_db, snr_db;
-  float* hk;                  // workspace [B][n_src][2][n] fractional-delay kernels
-  float* img;                 // workspace [B][n_src][2][n] per-mic source images
+  float* hk;                  // O(n^2) fallback workspace [B][n_src][2][n] delay kernels
+  float* img;                 // O(n^2) fallback workspace [B][n_src][2][n] source images
   float* mix;                 // [B][mix_stride]: mic channels at ch_stride
   long long mix_stride, ch_stride;
   float* tgt;                 // [B][ref_stride] mic-1 target image / peak
@@ -151,7 +151,12 @@ struct SceneArgs {
 }  // namespace avz
 
 extern "C" {
-int avz_launch_scene(const avz::SceneArgs* a, void* stream);
+int avz_launch_scene(const avz::SceneArgs* a, void* ws, void* stream);
+int avz_launch_scene_generate(avz::SceneArgs* a, long long start, uint32_t seed, void* ws,
+                              void* stream);
+long long avz_scene_mix_ws(int batch, int n_src, int n);
+int avz_scene_fft_len(int n);  // 1: n factors into 8, 4, 2, 5, 3 (the FFT path)
+long long avz_scene_gen_ws(int batch, int n_src, int n);
 int avz_launch_chunk_split(const avz::ChunkSplitArgs* a, void* stream);
 int avz_launch_metrics(const avz::MetricsArgs* a, void* stream);
 int avz_launch_chunk_merge(const avz::ChunkMergeArgs* a, void* stream);

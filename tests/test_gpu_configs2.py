@@ -3,7 +3,8 @@
 rt_av_zoom/core/world.py:116), oracle IBM, 1024/512, sigma 1 — through the sharded batch
 driver (avz.batch_run.run_batch, the Final_pipeline/batch_run.py:12-49 replacement, world
 size 1 here) and through MVDRPlan.run directly: the oracle on sampled utterances
-(waveform <= 1e-4, SIR |d| <= 0.01 dB), run-to-run determinism, and the CSV rows."""
+(waveform <= 1e-4, SIR |d| <= 0.01 dB), run-to-run determinism, and the CSV rows. The
+shard is generated on the device (avz_scene_generate, as run_batch does)."""
 import csv
 
 import numpy as np
@@ -20,14 +21,13 @@ B, S, N, K = 512, 64000, 1024, 3
 @pytest.fixture(scope="module")
 def shard(gpu_device):
     from avz import synth
-    mix, tgt, itf = synth.make_batch(B, start=0, n_samples=S, n_interferers=K)
-    d = lambda a: torch.from_numpy(a).to(gpu_device)  # noqa: E731
-    return mix, tgt, itf, d(mix), d(tgt), d(itf)
+    return synth.make_batch_device(B, start=0, n_samples=S, n_interferers=K, device=gpu_device,
+                                   rng="philox")
 
 
 def test_plan_run_matches_oracle_and_is_deterministic(shard):
     import avz
-    mix, tgt, itf, dm, dt, di = shard
+    dm, dt, di = shard
     plan = avz.MVDRPlan(n_fft=N, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
                         normalize="peak", max_batch=B, max_samples=S)
     out, peak = plan.run(dm, ref_tgt=dt, ref_int=di)
@@ -37,17 +37,18 @@ def test_plan_run_matches_oracle_and_is_deterministic(shard):
     n_out = plan.out_len(S)
     worst_w, worst_sir = 0.0, 0.0
     for b in (0, 1, 255, 384, 511):
-        ref = O.oracle_debug_vec(mix[b], tgt[b], itf[b], n_fft=N, hop=N // 2, sigma=1.0)
+        mix, tgt, itf = dm[b].cpu().numpy(), dt[b].cpu().numpy(), di[b].cpu().numpy()
+        ref = O.oracle_debug_vec(mix, tgt, itf, n_fft=N, hop=N // 2, sigma=1.0)
         got = out1[b, :n_out].cpu().numpy().astype(np.float64)
         worst_w = max(worst_w, float(np.max(np.abs(got - ref))))
-        d_sir = abs(O.projection_sdr_sir(got[:S], tgt[b], itf[b])[1]
-                    - O.projection_sdr_sir(ref[:S], tgt[b], itf[b])[1])
+        d_sir = abs(O.projection_sdr_sir(got[:S], tgt, itf)[1]
+                    - O.projection_sdr_sir(ref[:S], tgt, itf)[1])
         worst_sir = max(worst_sir, d_sir)
     print(f"configs[2] shard: worst waveform |d| {worst_w:.2e}, worst SIR |d| {worst_sir:.2e} dB")
     assert worst_w <= 1e-4 and worst_sir <= 0.01
 
 
-def test_run_batch_shard_rows_and_metrics(shard, gpu_device, tmp_path):
+def test_run_batch_shard_rows_and_metrics(gpu_device, tmp_path):
     """run_batch over the 512-utterance shard in one launch: one CSV row per utterance in
     batch_metrics.csv format, SIR sums equal to the per-row values, a positive mean SIR
     improvement (3 interferers at SIR 0 dB)."""
