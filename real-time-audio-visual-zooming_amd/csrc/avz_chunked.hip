@@ -258,6 +258,18 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     AVZ_STAMP(0);
 #endif
     if (live) {
+      if constexpr (MASK == MASK_IPD) {
+        // Bitwise-identical channel samples give bitwise-identical pocketfft spectra in the
+        // reference, hence equal angles (weight 0.01) in every bin of the frame; the packed
+        // FFT's split does not reproduce that equality, so the frame is flagged here.
+        bool same = true;
+        static_for<0, PPL>([&](auto r) {
+          same &= __float_as_uint(v[r].x) == __float_as_uint(v[r].y);
+        });
+        const unsigned long long nb = __ballot(!same);
+        const bool ident = (C::FPW == 1) ? nb == 0ull : ((nb >> (32 * lm.grp)) & 0xffffffffull) == 0ull;
+        if ((lane & (64 / C::FPW - 1)) == 0) lds[G::MISC_OFF + my_slot] = ident ? 1 : 0;
+      }
       if constexpr (std::is_same<TW, NoTw>::value)
         window_fft<N>(v, wc, fft, my_spec, twid, lm);
       else
@@ -274,6 +286,9 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     uint32_t ipd_fix[BPT];
 #pragma unroll
     for (int j = 0; j < BPT; ++j) ipd_fix[j] = 0u;
+    // IPD: frames whose two channels are bitwise identical (bit 8 i: slot i)
+    const unsigned long long ident_w =
+        (MASK == MASK_IPD) ? *reinterpret_cast<const unsigned long long*>(lds + G::MISC_OFF) : 0ull;
     const bool mask_vec = MASK == MASK_EXTERNAL && A.mask_st == 1 && (A.mask_sf & 3) == 0 &&
                           (A.mask_sb & 3) == 0 &&
                           ((reinterpret_cast<uintptr_t>(A.ext_mask) & 15) == 0) && (f0 & 3) == 0;
@@ -318,7 +333,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
               split_pair2(zm[i], zmp[i], x0, x1);  // 2 y0, 2 y1
               if constexpr (MASK == MASK_IPD) {
                 // the exact angle test of near-colinear bins runs after the loop
-                const bool clear = ipd_clear(x0, x1);
+                const bool clear = ipd_clear(x0, x1) && !((ident_w >> (8 * (g0 + i))) & 1ull);
                 ipd_fix[j] |= (clear ? 0u : 1u) << (g0 + i);
 #if AVZ_BINS_V1
                 const float w = clear ? 1.0f : 0.0f;
@@ -383,7 +398,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
           const cf* Zm = slot_ptr<N>(lds, i);
           cf x0, x1;
           split_pair2(Zm[kb], Zm[kp], x0, x1);
-          const float w = ipd_weight_exact(x0, x1);
+          const float w = ((ident_w >> (8 * i)) & 1ull) ? 0.01f : ipd_weight_exact(x0, x1);
           acc[j].add(x0, x1, w, w);
         }
       }
@@ -396,7 +411,8 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         split_pair2(Zm[N / 2], Zm[N / 2], y0, y1);
         if constexpr (MASK == MASK_IBM) zr = slot_ptr<N>(lds, FB + lane)[N / 2];
         float wn;
-        const float mn = bin_mask<MASK>(A, b, y0, y1, zr, zr, N / 2, f0 + lane, noise, wn);
+        float mn = bin_mask<MASK>(A, b, y0, y1, zr, zr, N / 2, f0 + lane, noise, wn);
+        if (MASK == MASK_IPD && ((ident_w >> (8 * lane)) & 1ull)) wn = mn = 0.01f;
         an.add(y0, y1, wn, mn);
         if constexpr (IRM) gain[(step * FB + lane) * F + N / 2] = irm_gain(zr, zr);
       }

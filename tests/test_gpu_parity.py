@@ -72,6 +72,29 @@ def test_stft_stage(avz, gpu_device, n):
 
 
 # ----------------------------------------------------------------------------- fused IBM
+def ibm_flip_report(name, cov, st):
+    """Mask fidelity of the IBM chain: per-bin noise-frame counts (cov_out column 4) against
+    the oracle's (pinned to the reference's stage_* goldens). Counts are exact except where
+    |S_int| ~ |S_tgt| to within fp32 FFT rounding (the GPU STFT is fp32; scipy's is fp64
+    rounded to complex64). FFT error scales with the frame's largest bin, so a flipped bin
+    must hold a tie relative to that scale; any other flip fails."""
+    msum = st["mask"].sum(axis=1)
+    diff = np.nonzero(cov[:, 4] != msum)[0]
+    assert len(diff) <= max(1, len(msum) // 100)
+    frame_scale = np.maximum(np.abs(st["S_i"]).max(axis=0), np.abs(st["S_t"]).max(axis=0))
+    margins = []
+    for k in diff:
+        a, b = np.abs(st["S_i"][k]), np.abs(st["S_t"][k])
+        rel = np.abs(a - b) / np.maximum(frame_scale, 1e-30)
+        margins.append(float(np.min(rel)))
+        assert np.min(rel) < 1e-5, (k, np.min(rel))
+    # mask fidelity: bins whose noise-frame count differs, and how close to a tie the
+    # closest (|S_int| - |S_tgt|) of each was; non-tie flips would have failed above
+    n_flip = int(np.sum(np.abs(cov[diff, 4] - msum[diff])))
+    print(f"{name}: IBM flips {n_flip} in {len(diff)}/{len(msum)} bins "
+          f"(all ties; max relative margin {max(margins, default=0.0):.1e}), non-tie flips 0")
+
+
 EXC = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "excerpt_*.npz")))
 FULL = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "full_*.npz")))
 
@@ -90,17 +113,8 @@ def test_fused_ibm_excerpt_vs_reference(avz, gpu_device, name):
     assert abs(peak - float(g["peak_raw"])) <= 1e-4 * float(g["peak_raw"])
     # stage parity against the oracle's fp64 covariance / weights
     _, st = O.oracle_debug_vec(mix, tgt, itf, n_fft=n, hop=n // 2, sigma=s, return_stages=True)
+    ibm_flip_report(name, cov, st)
     msum = st["mask"].sum(axis=1)
-    # IBM counts are exact except where |S_int| ~ |S_tgt| to within fp32 FFT rounding (the
-    # GPU STFT is fp32; scipy's is fp64 rounded to complex64). FFT error scales with the
-    # frame's largest bin, so a flipped bin must hold a tie relative to that scale.
-    diff = np.nonzero(cov[:, 4] != msum)[0]
-    assert len(diff) <= max(1, len(msum) // 100)
-    frame_scale = np.maximum(np.abs(st["S_i"]).max(axis=0), np.abs(st["S_t"]).max(axis=0))
-    for k in diff:
-        a, b = np.abs(st["S_i"][k]), np.abs(st["S_t"][k])
-        rel = np.abs(a - b) / np.maximum(frame_scale, 1e-30)
-        assert np.min(rel) < 1e-5, (k, np.min(rel))
     ok = cov[:, 4] == msum
     R = st["R"] * (msum + 1e-6)[:, None, None]
     scale = np.max(np.abs(R[:, 0, 0]))
@@ -117,14 +131,15 @@ def test_fused_ibm_full_length_vs_reference(avz, gpu_device, name):
     trip = name.split("_")[1]
     mix, tgt, itf = triple_f32(trip)
     n, s = int(g["n_fft"]), float(g["sigma"])
-    out, _ = run_ibm(avz, gpu_device, mix, tgt, itf, n, s)
+    out, _, cov, _ = run_ibm(avz, gpu_device, mix, tgt, itf, n, s, debug=True)
     assert len(out) == int(g["out_len"])
     assert np.max(np.abs(out[::16] - g["out_stride16"])) <= WAVE_TOL
     assert np.max(np.abs(out[:4096] - g["out_head"])) <= WAVE_TOL
     assert abs(sir(out, tgt, itf) - float(g["sir_out"])) <= SIR_TOL
     # full-array check against the oracle (identical inputs)
-    ref = O.oracle_debug_vec(mix, tgt, itf, n_fft=n, hop=n // 2, sigma=s)
+    ref, st = O.oracle_debug_vec(mix, tgt, itf, n_fft=n, hop=n // 2, sigma=s, return_stages=True)
     assert np.max(np.abs(out - ref)) <= WAVE_TOL
+    ibm_flip_report(name, cov, st)
 
 
 # ----------------------------------------------------------------------------- fused IPD
@@ -135,11 +150,22 @@ def test_fused_ipd_vs_reference(avz, gpu_device, trip, n):
     mix, tgt, itf = triple_f32(trip)
     plan = avz.MVDRPlan(n_fft=n, sigma=1e-7, mic_d=0.01, mask="ipd", postfilter="none",
                         normalize="peak", norm_eps=1e-6, max_batch=1, max_samples=len(tgt))
-    out, _ = plan.run(dev_t(mix, gpu_device)[None])
+    F = n // 2 + 1
+    cov = torch.zeros((1, F, 5), dtype=torch.float64, device=gpu_device)
+    out, _ = plan.run(dev_t(mix, gpu_device)[None], cov_out=cov)
     torch.cuda.synchronize()
     out = out[0, :plan.out_len(len(tgt))].cpu().numpy().astype(np.float64)
     assert len(out) == int(g["out_len"])
-    ref = O.masked_mvdr_vec(mix, n_fft=n, hop=n // 2)
+    ref, st = O.masked_mvdr_vec(mix, n_fft=n, hop=n // 2, return_stages=True)
+    # mask fidelity: per-bin weight sums (1 or 0.01 per frame) against the reference's;
+    # a (bin, frame) decided differently moves its bin's sum by 0.99
+    msum = cov[0, :, 4].cpu().numpy()
+    rsum = st["mask"].astype(np.float64).sum(axis=1)
+    dev = np.abs(msum - rsum)
+    n_dev = int(np.sum(np.round(dev / 0.99)))
+    print(f"ipd_{trip}_n{n}: IPD mask decisions differing from the reference: {n_dev} of "
+          f"{st['mask'].size} (max |sum diff| {dev.max():.2e})")
+    assert n_dev == 0
     assert np.max(np.abs(out - ref)) <= WAVE_TOL
     assert np.max(np.abs(out[::16] - g["out_stride16"])) <= WAVE_TOL
     assert abs(sir(out, tgt, itf) - float(g["sir_out"])) <= SIR_TOL
@@ -173,6 +199,15 @@ def test_fused_external_mask(avz, gpu_device, n, floor):
     torch.cuda.synchronize()
     got2 = out2[0, :len(ref)].cpu().numpy()
     assert np.max(np.abs(got2 - ref)) <= WAVE_TOL * scale
+    # t-contiguous rows padded to a multiple of 4 frames (16-B aligned row starts) while T
+    # itself is not: 16-B row-segment reads on the full steps, scalar reads on the last
+    T = M.shape[1]
+    Mp = np.zeros((M.shape[0], -(-T // 4) * 4), np.float32)
+    Mp[:, :T] = M
+    out3, _ = plan.run(dev_t(mix, gpu_device)[None], ext_mask=dev_t(Mp, gpu_device)[None, :, :T])
+    torch.cuda.synchronize()
+    got3 = out3[0, :len(ref)].cpu().numpy()
+    assert np.max(np.abs(got3 - ref)) <= WAVE_TOL * scale
 
 
 # ----------------------------------------------------------------------------- batching
@@ -217,13 +252,10 @@ def test_plan_rejects_bad_shapes(avz, gpu_device):
 # ----------------------------------------------------------------------------- IPD ties
 def test_ipd_identical_channels(avz, gpu_device):
     """Degenerate IPD input: both channels identical, so masked_mvdr.py:37-46 sees
-    bitwise-equal angles in every bin and weights them all 0.01. The HIP path transforms
-    the two channels as one packed complex FFT, whose split does not reproduce
-    bitwise-equal channel spectra: every (bin, frame) reaches the exact-angle fix-up
-    pass and most come out 1.0 (documented deviation; measured: mask sums
-    ~100x the reference's). The output is unaffected — with identical channels R is
-    rank one and the MVDR weights at broadside do not depend on the mask weighting —
-    and is checked against the oracle at the usual tolerance."""
+    bitwise-equal angles in every bin and weights them all 0.01. The packed FFT's split
+    does not reproduce bitwise-equal channel spectra, so the analysis kernel flags frames
+    whose two channels are bitwise identical and gives every bin of them the reference's
+    0.01: the per-bin mask sums equal the reference's, and the output the oracle's."""
     mix, tgt, itf = triple_f32("test")
     n = 1024
     mono = np.ascontiguousarray(np.stack([mix[0], mix[0]]))
@@ -237,7 +269,25 @@ def test_ipd_identical_channels(avz, gpu_device):
     ref, st = O.masked_mvdr_vec(mono, n_fft=n, hop=n // 2, return_stages=True)
     # sum of mask weights per bin (cov column 4) vs the reference's
     msum = cov[0, :, 4].cpu().numpy()
-    rsum = st["mask"].sum(axis=1)
+    rsum = st["mask"].astype(np.float64).sum(axis=1)
     print(f"identical channels: max |mask sum - ref| = {np.max(np.abs(msum - rsum)):.3g} "
           f"(ref sum per bin {rsum[10]:.3g}), max |out - ref| = {np.max(np.abs(out - ref)):.3g}")
+    np.testing.assert_allclose(msum, rsum, rtol=1e-6)
     assert np.max(np.abs(out - ref)) <= WAVE_TOL
+    # one channel differing in a single sample: only the frames that see it leave the flag;
+    # there the two spectra differ by a tiny amount, so bins whose reference angles agree to
+    # within fp32 rounding are genuine ties (decided by the last bit of each STFT)
+    mono2 = mono.copy()
+    mono2[1, 20000] += 1e-3
+    out2, _ = plan.run(dev_t(mono2, gpu_device)[None], cov_out=cov)
+    torch.cuda.synchronize()
+    _, st2 = O.masked_mvdr_vec(mono2, n_fft=n, hop=n // 2, return_stages=True)
+    msum2 = cov[0, :, 4].cpu().numpy()
+    rsum2 = st2["mask"].astype(np.float64).sum(axis=1)
+    dev_bins = np.nonzero(np.round(np.abs(msum2 - rsum2) / 0.99))[0]
+    ang = np.angle(st2["Y"].astype(np.complex128))
+    dphi = np.abs(np.angle(np.exp(1j * (ang[0] - ang[1]))))  # [F, T]
+    for k in dev_bins:
+        assert np.min(dphi[k][dphi[k] > 0], initial=0.0) < 1e-6, (k, np.min(dphi[k]))
+    print(f"one differing sample: mask decisions differing from the reference: "
+          f"{len(dev_bins)} bins, all angle ties (|d angle| < 1e-6 rad)")
