@@ -71,6 +71,10 @@ def parse():
                     help="STFT size (hop n/2); 1024 is the BASELINE configs, 512 oracle_debug's default")
     ap.add_argument("--unet-dtype", choices=("fp32", "bf16"), default="fp32",
                     help="unet workload: U-Net forward precision (fp32 = the reference's)")
+    ap.add_argument("--normalize", choices=("peak", "deferred"), default="peak",
+                    help="ibm/ipd: peak normalisation in HBM (the reference's output, the "
+                         "headline) or deferred to the consumer (the batch driver's form: "
+                         "un-normalised output + peak[B], no rescale pass)")
     ap.add_argument("--scenes", choices=("philox", "host"), default="philox",
                     help="input scenes: generated on the device (avz_scene_generate) or the "
                          "host numpy generator (make_batch)")
@@ -147,13 +151,14 @@ def setup_chain(args, B, S, dev, d_mix, d_tgt, d_itf):
     import torch
 
     import avz
+    norm = "peak" if args.normalize == "peak" else "none"
     if args.workload == "ibm":
         plan = avz.MVDRPlan(n_fft=N_FFT, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
-                            normalize="peak", max_batch=B, max_samples=S)
+                            normalize=norm, max_batch=B, max_samples=S)
         streams = 4
     else:
         plan = avz.MVDRPlan(n_fft=N_FFT, sigma=1e-7, mic_d=0.01, mask="ipd", postfilter="none",
-                            normalize="peak", norm_eps=1e-6, max_batch=B, max_samples=S)
+                            normalize=norm, norm_eps=1e-6, max_batch=B, max_samples=S)
         streams = 2
     refs = {}
     if args.workload == "ibm":
@@ -167,7 +172,7 @@ def setup_chain(args, B, S, dev, d_mix, d_tgt, d_itf):
 
     n_out = plan.out_len(S)
     F, T = N_FFT // 2 + 1, -(-S // HOP) + 1
-    info = dict(plan=plan, out=out[:, :min(n_out, S)], bins=B * F * T,
+    info = dict(plan=plan, out=out[:, :min(n_out, S)], peak=peak, bins=B * F * T,
                 alg_analysis=B * streams * S * 4, alg_chain=B * (streams * S * 4 + n_out * 4),
                 kernel=f"avz_analysis_kernel<{N_FFT},{'IBM' if args.workload == 'ibm' else 'IPD'}>",
                 mix=d_mix, refs=refs)
@@ -345,7 +350,12 @@ def main():
         L = est_out.shape[1]
     d_tgt, d_itf = d_tgt[:, :L], d_itf[:, :L]
     est = torch.cat([est_out, d_mix[:, 0, :L]])
-    m = metrics.projection_metrics(est, torch.cat([d_tgt] * 2), torch.cat([d_itf] * 2))
+    est_peak = None
+    if args.workload != "unet" and args.normalize == "deferred":  # score out / peak
+        eps = 1e-6 if args.workload == "ipd" else 0.0
+        est_peak = torch.cat([info["peak"] + eps, torch.ones_like(info["peak"])])
+    m = metrics.projection_metrics(est, torch.cat([d_tgt] * 2), torch.cat([d_itf] * 2),
+                                   est_peak=est_peak)
     sir_out, sir_in = m[:B, 3], m[B:, 3]
     sums = torch.stack([sir_in.sum(), sir_out.sum(), torch.tensor(float(B), device=dev,
                                                                   dtype=torch.float64)])
@@ -388,7 +398,8 @@ def main():
     if os.path.exists(tf) and args.workload == "ibm":
         pm = json.load(open(tf))
         if pm.get("batch") == B and pm.get("n_fft") == N_FFT and pm.get("samples") == S:
-            traffic = pm.get("hbm_bytes_per_launch", {})
+            key = "hbm_bytes_per_launch" if args.normalize == "peak" else "deferred_hbm_bytes_per_launch"
+            traffic = pm.get(key, {})
             if not isinstance(traffic, dict):
                 traffic = {}
     achieved = value / world * bpb / 1e9
@@ -425,10 +436,10 @@ def main():
                f"utterance-sharded x{world}, RCCL metric all-reduce only"}
         if args.workload == "ibm":
             cfg.update(tf_bins_per_utt=info["bins"] // B, sigma=1.0, mask="ibm",
-                       postfilter="ibm", normalize="peak")
+                       postfilter="ibm", normalize=args.normalize)
         elif args.workload == "ipd":
             cfg.update(tf_bins_per_utt=info["bins"] // B, sigma=1e-7, mask="ipd",
-                       postfilter="none", normalize="peak")
+                       postfilter="none", normalize=args.normalize)
         else:
             cfg.update(chunk_items=info["n_items"], tf_bins_per_chunk=info["bins"] // info["n_items"],
                        sigma=1e-5, mask="external (U-Net)", postfilter="max(M, 0.05)",

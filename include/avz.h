@@ -279,6 +279,14 @@ int avz_projection_metrics(int batch, int max_len, const int* len, const float* 
                            long long est_stride, const float* tgt, long long tgt_stride,
                            const float* itf, long long itf_stride, double* sums,
                            double* metrics, void* hip_stream);
+/* The same metrics of est[b] / (est_peak[b] + est_eps): an un-normalised output (a plan
+ * with AVZ_NORM_NONE, whose peak[] it returns) scored as the peak-normalised one without
+ * the normalisation pass over the samples (the scale enters the fp64 sums). */
+int avz_projection_metrics_scaled(int batch, int max_len, const int* len, const float* est,
+                                  long long est_stride, const float* est_peak, double est_eps,
+                                  const float* tgt, long long tgt_stride, const float* itf,
+                                  long long itf_stride, double* sums, double* metrics,
+                                  void* hip_stream);
 
 /* Synthetic scene mixing on the device — the anechoic far-field generator of
  * full_audio_generating_pipeline/world_building.py:47-59 (per-mic fractional delay by an

@@ -39,6 +39,7 @@ EXPORTED = [
     "avz_last_hip_error", "avz_version", "avz_mvdr_workspace_bytes",
     "avz_mvdr_covariance", "avz_solve_covariance", "avz_apply_istft", "avz_beamform_spectral",
     "avz_istft", "avz_scene_generate_workspace_bytes", "avz_scene_generate",
+    "avz_projection_metrics_scaled",
 ]
 
 
@@ -135,6 +136,7 @@ def _load():
     D = ct.c_double
     lib.avz_srp_scan.argtypes = [P, I, P, I, P, LL, LL, I, D, D, D, D, P, P]
     lib.avz_projection_metrics.argtypes = [I, I, P, P, LL, P, LL, P, LL, P, P, P]
+    lib.avz_projection_metrics_scaled.argtypes = [I, I, P, P, LL, P, D, P, LL, P, LL, P, P, P]
     lib.avz_scene_workspace_bytes.argtypes = [I, I, I]
     lib.avz_scene_workspace_bytes.restype = LL
     lib.avz_scene_mix.argtypes = [I, I, I, P, P, P, D, D, D, D, D, P, LL, LL, P, P, LL, P, LL, P]
@@ -149,7 +151,7 @@ def _load():
                  "avz_mvdr_batch", "avz_stft", "avz_chunk_split", "avz_chunk_merge",
                  "avz_plan_set_timing", "avz_plan_get_timing", "avz_mask_features",
                  "avz_srp_scan", "avz_projection_metrics", "avz_scene_mix",
-                 "avz_scene_generate", "avz_version"):
+                 "avz_scene_generate", "avz_projection_metrics_scaled", "avz_version"):
         getattr(lib, name).restype = ct.c_int
     return lib
 

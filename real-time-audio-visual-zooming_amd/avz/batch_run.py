@@ -55,16 +55,24 @@ class BatchResult:
 
 
 def gpu_enhancer(n_fft=1024, sigma=1.0, mic_d=0.01, max_batch=256, max_samples=64000,
-                 device=None) -> Callable:
-    """Returns enhance(mix[B,2,S], tgt[B,S], itf[B,S]) -> out[B, S_out] (device tensors)
-    backed by one avz_mvdr_batch launch (oracle IBM, IBM post-filter, peak-normalised)."""
+                 device=None, normalize="deferred") -> Callable:
+    """Returns enhance(mix[B,2,S], tgt[B,S], itf[B,S]) backed by one avz_mvdr_batch launch
+    (oracle IBM, IBM post-filter) over device tensors.
+
+    normalize="peak":     -> out[B, S_out], peak-normalised in HBM (the finalize kernel's
+                          rescale pass re-reads and re-writes every sample);
+    normalize="deferred": -> (out, peak): the un-normalised output and its peak; the
+                          consumer applies 1 / peak (the metrics fold it into their fp64
+                          sums), which skips that pass — the batch driver's default."""
     from .engine import MVDRPlan
     plan = MVDRPlan(n_fft=n_fft, sigma=sigma, mic_d=mic_d, mask="ibm", postfilter="ibm",
-                    normalize="peak", max_batch=max_batch, max_samples=max_samples)
+                    normalize="none" if normalize == "deferred" else normalize,
+                    max_batch=max_batch, max_samples=max_samples)
 
     def enhance(mix, tgt, itf):
-        out, _ = plan.run(mix, ref_tgt=tgt, ref_int=itf)
-        return out[:, :plan.out_len(mix.shape[-1])]
+        out, peak = plan.run(mix, ref_tgt=tgt, ref_int=itf)
+        out = out[:, :plan.out_len(mix.shape[-1])]
+        return (out, peak) if normalize == "deferred" else out
     return enhance
 
 
@@ -97,9 +105,13 @@ def run_batch(n_runs: int, start_idx: int = 0, n_interferers: int = 2, *,
             d_tgt = torch.from_numpy(tgt).to(dev)
             d_itf = torch.from_numpy(itf).to(dev)
         out = enhance(d_mix, d_tgt, d_itf)
+        peak = None
+        if isinstance(out, tuple):  # deferred normalisation: (un-normalised out, peak)
+            out, peak = out
         L = min(out.shape[-1], S)
         osinr_b, osir_b = metrics.calculate_osnr_osir(d_mix[:, 0, :L], d_tgt[:, :L], d_itf[:, :L])
-        osinr_s, osir_s = metrics.calculate_osnr_osir(out[:, :L], d_tgt[:, :L], d_itf[:, :L])
+        osinr_s, osir_s = metrics.calculate_osnr_osir(out[:, :L], d_tgt[:, :L], d_itf[:, :L],
+                                                      peak=peak)
         sums += torch.stack([osir_b.sum(), osir_s.sum(), osinr_b.sum(), osinr_s.sum(),
                              torch.tensor(float(nb), dtype=torch.float64, device=dev)])
         vals = torch.stack([osir_b, osir_s, osinr_b, osinr_s]).cpu().numpy()

@@ -32,8 +32,10 @@ CSV_HEADER = ["Run_ID", "SIR_Base", "SIR_Enh", "SIR_Imp", "SINR_Base", "SINR_Enh
 
 # ----------------------------------------------------------------------------- device path
 def projection_metrics(est: torch.Tensor, tgt: torch.Tensor, itf: torch.Tensor, lengths=None,
-                       stream=None):
-    """HIP: -> float64 [B, 4] = (OSINR, OSIR, SDR, SIR) per row, in dB."""
+                       stream=None, est_peak: torch.Tensor | None = None, est_eps: float = 0.0):
+    """HIP: -> float64 [B, 4] = (OSINR, OSIR, SDR, SIR) per row, in dB. With ``est_peak``
+    the rows are scored as est / (est_peak + est_eps) (an un-normalised output and its
+    peak, as a NORM_NONE plan returns them), the scale applied inside the fp64 sums."""
     from ._lib import check, lib
     from .engine import _stream_handle
     est, tgt, itf = (x.float().contiguous() if x.dtype != torch.float32 or x.stride(-1) != 1
@@ -49,6 +51,15 @@ def projection_metrics(est: torch.Tensor, tgt: torch.Tensor, itf: torch.Tensor, 
     sums = torch.empty((B, 6), dtype=torch.float64, device=dev)
     out = torch.empty((B, 4), dtype=torch.float64, device=dev)
     p = lambda t: ct.c_void_p(t.data_ptr())  # noqa: E731
+    if est_peak is not None:
+        pk = est_peak.float().contiguous()
+        assert pk.numel() == B and pk.device == dev
+        check(lib.avz_projection_metrics_scaled(B, L, p(lengths), p(est), est.stride(0), p(pk),
+                                                float(est_eps), p(tgt), tgt.stride(0), p(itf),
+                                                itf.stride(0), p(sums), p(out),
+                                                _stream_handle(stream)),
+              "avz_projection_metrics_scaled")
+        return out
     check(lib.avz_projection_metrics(B, L, p(lengths), p(est), est.stride(0), p(tgt),
                                      tgt.stride(0), p(itf), itf.stride(0), p(sums), p(out),
                                      _stream_handle(stream)), "avz_projection_metrics")
@@ -101,11 +112,14 @@ def calculate_metrics_manual(output, target, interf, lengths=None):
     return _host_manual(output, target, interf, lengths)
 
 
-def calculate_osnr_osir(output, target, interf, lengths=None):
-    """Batched Final_pipeline/src/metrics.calculate_osnr_osir -> (osinr [B], osir [B])."""
+def calculate_osnr_osir(output, target, interf, lengths=None, peak=None, eps=0.0):
+    """Batched Final_pipeline/src/metrics.calculate_osnr_osir -> (osinr [B], osir [B]).
+    ``peak``: score output / (peak + eps) (an un-normalised output and its peak)."""
     if output.is_cuda:
-        m = projection_metrics(output, target, interf, lengths)
+        m = projection_metrics(output, target, interf, lengths, est_peak=peak, est_eps=eps)
         return m[:, 0], m[:, 1]
+    if peak is not None:
+        output = output.double() / (peak.double()[:, None] + eps)
     return _host_osnr_osir(output, target, interf, lengths)
 
 

@@ -734,11 +734,12 @@ extern "C" int avz_scene_generate(int batch, long long start_idx, int n_interfer
   return rc;
 }
 
-extern "C" int avz_projection_metrics(int batch, int max_len, const int* len, const float* est,
-                                      long long est_stride, const float* tgt,
-                                      long long tgt_stride, const float* itf,
-                                      long long itf_stride, double* sums, double* metrics,
-                                      void* stream) {
+extern "C" int avz_projection_metrics_scaled(int batch, int max_len, const int* len,
+                                             const float* est, long long est_stride,
+                                             const float* est_peak, double est_eps,
+                                             const float* tgt, long long tgt_stride,
+                                             const float* itf, long long itf_stride,
+                                             double* sums, double* metrics, void* stream) {
   if (batch < 0 || max_len < 0) return AVZ_ERR_SHAPE;
   if (batch == 0) return AVZ_OK;
   if (!len || !est || !tgt || !itf || !sums || !metrics) return AVZ_ERR_ARG;
@@ -756,7 +757,18 @@ extern "C" int avz_projection_metrics(int batch, int max_len, const int* len, co
   m.itf_stride = itf_stride;
   m.sums = sums;
   m.metrics = metrics;
+  m.est_peak = est_peak;
+  m.est_eps = est_eps;
   const int rc = avz_launch_metrics(&m, stream);
   if (rc == AVZ_ERR_HIP) g_last_hip = hipGetErrorString(hipGetLastError());
   return rc;
+}
+
+extern "C" int avz_projection_metrics(int batch, int max_len, const int* len, const float* est,
+                                      long long est_stride, const float* tgt,
+                                      long long tgt_stride, const float* itf,
+                                      long long itf_stride, double* sums, double* metrics,
+                                      void* stream) {
+  return avz_projection_metrics_scaled(batch, max_len, len, est, est_stride, nullptr, 0.0, tgt,
+                                       tgt_stride, itf, itf_stride, sums, metrics, stream);
 }

@@ -107,6 +107,8 @@ struct MetricsArgs {
   long long est_stride, tgt_stride, itf_stride;
   double* sums;               // [B][6] workspace
   double* metrics;            // [B][4] OSINR, OSIR, SDR, SIR (dB)
+  const float* est_peak;      // [B] or null: score est / (est_peak[b] + est_eps)
+  double est_eps;
 };
 
 struct ChunkSplitArgs {

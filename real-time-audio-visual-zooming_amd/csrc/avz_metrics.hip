@@ -98,7 +98,9 @@ __global__ void avz_metrics_final_kernel(MetricsArgs A) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= A.batch) return;
   const double* s = A.sums + (long long)b * 6;
-  const double oo = s[0], tt = s[1], ii = s[2], ot = s[3], oi = s[4], ti = s[5];
+  // an un-normalised output scored as the peak-normalised one: o -> c o in the sums
+  const double c = A.est_peak ? 1.0 / ((double)A.est_peak[b] + A.est_eps) : 1.0;
+  const double oo = s[0] * c * c, tt = s[1], ii = s[2], ot = s[3] * c, oi = s[4] * c, ti = s[5];
   const double eps = 1e-10;
   const double nt = sqrt(tt) + eps, ni = sqrt(ii) + eps, no = sqrt(oo) + eps;
   // metrics.py:102-123: t^ = t/(|t|+eps), i^ = i/(|i|+eps); alpha = <o,t^>, beta = <o,i^>

@@ -10,7 +10,8 @@ that factor is applied here. `analysis_read_check` = 2 x FETCH_SIZE of the analy
 over its compulsory input bytes (2 mic + 2 reference streams) shows how tight it is.
 Writes are taken as reported.
 
-  python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv>
+  python tools/pmc_traffic.py <fetch csv> <write csv> [<fetch csv> <write csv> of the
+                               bench with --normalize deferred: the batch-driver path]
 """
 import csv
 import json
@@ -52,6 +53,14 @@ def main():
            "alg_bytes_per_launch": {"analysis": alg_reads, "chain": alg_reads + B * n_out * 4},
            "note": "reads = 2 x FETCH_SIZE (gfx950 half-count, calibrated in profiles/r01); "
                    "writes = WRITE_SIZE"}
+    if len(sys.argv) >= 5:  # the batch-driver path: normalisation deferred to the consumer
+        f2 = per_dispatch(sys.argv[3], "FETCH_SIZE")
+        w2 = per_dispatch(sys.argv[4], "WRITE_SIZE")
+        h2 = {k: (factor * f2[k] + w2[k]) * 1024 for k in KERNELS}
+        h2["chain"] = sum(h2.values())
+        out["deferred_hbm_bytes_per_launch"] = h2
+        out["deferred_chain_over_alg"] = h2["chain"] / out["alg_bytes_per_launch"]["chain"]
+    out["chain_over_alg"] = hbm["chain"] / out["alg_bytes_per_launch"]["chain"]
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1))

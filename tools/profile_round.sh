@@ -16,9 +16,15 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc_fet
   -- python3 bench.py --no-cpu --steps 5 --warmup 2 --no-kernel-timing > $out/pmc_fetch.log 2>&1 || { tail -20 $out/pmc_fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write -o run \
   -- python3 bench.py --no-cpu --steps 5 --warmup 2 --no-kernel-timing > $out/pmc_write.log 2>&1 || { tail -20 $out/pmc_write.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc_fetch_d -o run \
+  -- python3 bench.py --no-cpu --steps 5 --warmup 2 --no-kernel-timing --normalize deferred > $out/pmc_fetch_d.log 2>&1 || { tail -20 $out/pmc_fetch_d.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write_d -o run \
+  -- python3 bench.py --no-cpu --steps 5 --warmup 2 --no-kernel-timing --normalize deferred > $out/pmc_write_d.log 2>&1 || { tail -20 $out/pmc_write_d.log; exit 1; }
 f1=$(find $out/pmc_fetch -name "*counter_collection.csv" | head -1)
 f2=$(find $out/pmc_write -name "*counter_collection.csv" | head -1)
-python3 tools/pmc_traffic.py "$f1" "$f2" > $out/pmc_traffic.log 2>&1 || { cat $out/pmc_traffic.log; exit 1; }
+f3=$(find $out/pmc_fetch_d -name "*counter_collection.csv" | head -1)
+f4=$(find $out/pmc_write_d -name "*counter_collection.csv" | head -1)
+python3 tools/pmc_traffic.py "$f1" "$f2" "$f3" "$f4" > $out/pmc_traffic.log 2>&1 || { cat $out/pmc_traffic.log; exit 1; }
 cp profiles/pmc_traffic.json $out/
 timeout -k 10 300 python bench.py --no-cpu > $out/bench_traffic.log 2>&1 || { tail -20 $out/bench_traffic.log; exit 1; }
 tail -1 $out/bench_traffic.log
