@@ -531,8 +531,121 @@ __global__ void __launch_bounds__(NT, 2) bench_pairs_glds(const float* in, float
   out[blockIdx.x * NT + threadIdx.x] = a;
 }
 
+
+// One 1024-point FFT per wave, 16 points per lane, three register passes and two LDS
+// transposes, no cross-lane instructions: 1024 = 16 (r) x 64 (L), the 64-point DFT over L
+// split as L = u + 4 w (DFT-16 over w, then DFT-4 over u).
+//   in : lane L, reg r <-> x[L + 64 r]
+//   out: lane (k1 = L & 15, q = L >> 4), reg 4 i + j <-> X[k1 + 64 q + 16 i + 256 j]
+// Scratch: 16 x 68 float2 (8.7 KB) per wave, conflict-free for both transposes.
+struct Fft1024p3 {
+  cf twa[15];  // W1024^{L k1}, k1 = 1..15
+  cf twb[15];  // W64^{u k2}, u = L >> 4, k2 = 1..15
+  int lane;
+  __device__ __forceinline__ void init(int ln) {
+    lane = ln;
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      twa[k - 1] = unit_root((double)(ln * k) / 1024.0);
+      twb[k - 1] = unit_root((double)((ln >> 4) * k) / 64.0);
+    }
+  }
+  __device__ __forceinline__ void forward(cf (&v)[16], cf* scr) const {
+    dft16(v);
+    static_for<1, 16>([&](auto k) { v[k] = c_mul(v[k], twa[k - 1]); });
+    static_for<0, 16>([&](auto k) { scr[k * 66 + lane] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    {
+      const int k1 = lane & 15, u = lane >> 4;
+      static_for<0, 16>([&](auto w) { v[w] = scr[k1 * 66 + u + 4 * w]; });
+    }
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    static_for<1, 16>([&](auto k) { v[k] = c_mul(v[k], twb[k - 1]); });
+    static_for<0, 16>([&](auto k) { scr[k * 68 + lane] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    {
+      const int k1 = lane & 15, q = lane >> 4;
+      static_for<0, 4>([&](auto i) {
+        static_for<0, 4>([&](auto u) { v[4 * i + u] = scr[(4 * q + i) * 68 + 16 * u + k1]; });
+      });
+    }
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 4>([&](auto i) { dft4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]); });
+  }
+};
+
+// Fft1024p3 (16 points per lane, one FFT per wave, two transposes, no cross-lane ops).
+// MODE 0: FFT only; MODE 1: + natural-order spectrum store and wave-local re-read.
+template <int MODE>
+__global__ void __launch_bounds__(256, 4) bench_p3(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  Fft1024p3 f; f.init(lane);
+  cf* scr = reinterpret_cast<cf*>(lds + wave * 8704);
+  cf v[16];
+  static_for<0, 16>([&](auto r) { v[r] = {in[(64 * r + lane) & 1023], in[(64 * r + lane + 3) & 1023]}; });
+  for (int it = 0; it < iters; ++it) {
+    f.forward(v, scr);
+    if constexpr (MODE == 1) {
+      const int k1 = lane & 15, q = lane >> 4;
+      static_for<0, 16>([&](auto r) { scr[k1 + 64 * q + 16 * (r >> 2) + 256 * (r & 3)] = v[r]; });
+      __builtin_amdgcn_wave_barrier();
+      static_for<0, 16>([&](auto r) { v[r] = scr[(lane + 64 * r) & 1023]; });
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  float acc = 0;
+  static_for<0, 16>([&](auto k) { acc += v[k].x + v[k].y; });
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+// Fft1024 (x1: 16 points per lane with permlane32 radix-2), FFT only, 4 waves per SIMD.
+__global__ void __launch_bounds__(256, 4) bench_x1only(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  Fft1024 f; f.init(lane);
+  cf* scr = reinterpret_cast<cf*>(lds + wave * 8448);
+  cf v[16];
+  static_for<0, 16>([&](auto r) { v[r] = {in[(64 * r + lane) & 1023], in[(64 * r + lane + 3) & 1023]}; });
+  for (int it = 0; it < iters; ++it) f.forward(v, scr);
+  float acc = 0;
+  static_for<0, 16>([&](auto k) { acc += v[k].x + v[k].y; });
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+// x2 FFT only, 8 waves per block (two per SIMD: waves w and w + 4 share one); OFFSET: the
+// upper four waves run one extra stage-2 DFT first, so the two waves of a SIMD are half an
+// FFT out of phase (one in its LDS transpose while the other computes).
+template <bool OFFSET>
+__global__ void __launch_bounds__(512, 1) bench_x2_phase(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 5, l = lane & 31;
+  cf* tw = reinterpret_cast<cf*>(lds + 8 * 16896);
+  Fft1024x2::fill_twiddles(tw, threadIdx.x, 512);
+  Fft1024x2 f; f.init(lane);
+  cf* scr = reinterpret_cast<cf*>(lds + wave * 16896 + g * 8448);
+  cf v[32];
+  static_for<0, 32>([&](auto r) { v[r] = {in[(l + 32 * r) & 1023], in[(l + 32 * r + 7) & 1023]}; });
+  __syncthreads();
+  if (OFFSET && wave >= 4) f.stage2(v);
+  for (int it = 0; it < iters; ++it) f.forward(v, scr, tw);
+  float acc = 0;
+  static_for<0, 32>([&](auto k) { acc += v[k].x + v[k].y; });
+  out[blockIdx.x * 512 + threadIdx.x] = acc;
+}
+
 extern "C" int run_bench(int variant, const float* in, float* out, int blocks, int iters) {
   switch (variant) {
+    case 26: case 27: { auto k = variant == 26 ? bench_x2_phase<false> : bench_x2_phase<true>;
+      int lds = 8 * 16896 + 8192;
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, 0, in, out, iters); break; }
+    case 23: case 24: { auto k = variant == 23 ? bench_p3<0> : bench_p3<1>; int lds = 4 * 8704;
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
+    case 25: { auto k = bench_x1only; int lds = 4 * 8448;
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
     case 0: { auto k = bench_x2<512>; int lds = 8 * 16896 + 8192;
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, 0, in, out, iters); break; }

@@ -22,9 +22,14 @@ names = {0: "x2 (32 pts/lane), 8 waves/block", 1: "x1 (16 pts/lane), 16 waves/bl
          16: "current + loads not feeding the FFT", 17: "current + dwordx2 loads (same bytes)",
          18: "current + one channel's loads", 19: "current + 1/8 of the loads",
          20: "LDS tw, one channel's loads, two steps ahead", 21: "LDS tw, one channel's loads, one step ahead",
-         22: "pairs + LDS-DMA staged frames (4 streams)"}
-ffts_per_block = {0: 16, 1: 16, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 8, 9: 8, 10: 8, 11: 8, 12: 8, 13: 8, 14: 8, 15: 8, 16: 8, 17: 8, 18: 8, 19: 8, 20: 8, 21: 8, 22: 8}
-for v, blocks in ((13, 512), (14, 512), (10, 512), (22, 512), (13, 512), (14, 512), (10, 512), (22, 512)):
+         22: "pairs + LDS-DMA staged frames (4 streams)",
+         23: "p3 FFT only (16 pts/lane, 2 transposes), 4 w/b x4", 24: "p3 + wave-local spectrum round trip",
+         25: "x1 FFT only (permlane32), 4 w/b x4",
+         26: "x2 FFT only, 8 w/b, waves in phase", 27: "x2 FFT only, 8 w/b, SIMD pairs half an FFT apart"}
+ffts_per_block = {26: 16, 27: 16, 23: 4, 24: 4, 25: 4, 0: 16, 1: 16, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 8, 9: 8, 10: 8, 11: 8, 12: 8, 13: 8, 14: 8, 15: 8, 16: 8, 17: 8, 18: 8, 19: 8, 20: 8, 21: 8, 22: 8}
+import sys
+VARS = [(int(a.split(':')[0]), int(a.split(':')[1])) for a in sys.argv[1:]] or [(4, 512), (23, 1024), (24, 1024), (25, 1024)]
+for v, blocks in VARS:
     for _ in range(2):
         lib.run_bench(v, inp.data_ptr(), out.data_ptr(), blocks, iters)
     torch.cuda.synchronize()
