@@ -32,6 +32,9 @@
 #ifndef AVZ_BINS_V1
 #define AVZ_BINS_V1 0
 #endif
+#ifndef AVZ_REFBITS
+#define AVZ_REFBITS 1
+#endif
 
 namespace avz {
 
@@ -93,6 +96,37 @@ __device__ __forceinline__ void window_fft_reg(cf (&v)[32], const WinCoef<1024>&
   });
   fft.forward_reg(v, spec, tw_reg);
   static_for<0, 32>([&](auto k) { spec[lm.out0 + 32 * k] = v[k]; });
+}
+
+// Reference pair of the IBM mask (N = 1024, register twiddles): the reference spectrum is
+// only needed for one bit per bin, noise <=> Re(Zr[k] Zr[N - k]) < 0 (ibm_noise). Lane l
+// holds Zr[l + 32 k]; it stores its upper-half bins (k >= 16) to LDS, reads back the
+// partners N - (l + 32 k) of its lower-half bins (all in the upper half: (32 - l) +
+// 32 (31 - k), or 32 (32 - k) on lane 0; DC pairs with itself) and publishes the 16 bits
+// of bins l + 32 k, k < 16, as word l of the slot (bytes 0..127, below the stored bins).
+// The Nyquist bin (lane 0, k = 16) stays readable at spec[N / 2].
+__device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCoef<1024>& wc,
+                                                        const Fft1024x2& fft, cf* spec,
+                                                        const cf (&tw_reg)[31],
+                                                        const LaneMap<1024>& lm) {
+  constexpr int N = 1024;
+  static_for<0, 32>([&](auto r) {
+    constexpr float cr = W32::c[r], sr = -W32::s[r];
+    const float w = fmaf(wc.as, sr, fmaf(-wc.ac, cr, wc.a0));
+    v[r] = c_scale(v[r], w);
+  });
+  fft.forward_reg(v, spec, tw_reg);
+  const int l = lm.out0;
+  static_for<16, 32>([&](auto k) { spec[l + 32 * k] = v[k]; });
+  __builtin_amdgcn_wave_barrier();
+  uint32_t w = 0u;
+  static_for<0, 16>([&](auto k) {
+    const int m = l + 32 * k;
+    cf zp = spec[(N - m) & (N - 1)];
+    if (k == 0 && l == 0) zp = v[0];  // DC: its own partner (index 0 is not stored)
+    w |= (ibm_noise(v[k], zp) ? 1u : 0u) << k;
+  });
+  reinterpret_cast<uint32_t*>(spec)[l] = w;
 }
 
 template <int N>
@@ -176,6 +210,10 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
   constexpr int FB = (MASK == MASK_IBM) ? NSLOT / 2 : NSLOT;  // frames per step
   static_assert(kChunk % FB == 0, "steps tile the chunk");
+  // IBM without the IRM gains: the reference waves publish per-bin noise bits
+  // (window_fft_reg_ibm_bits) instead of the whole reference spectrum
+  constexpr bool REFBITS = AVZ_REFBITS && !AVZ_BINS_V1 && N == 1024 && MASK == MASK_IBM && !IRM &&
+                           !std::is_same<TW, NoTw>::value;
 
   cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
   const int tid = threadIdx.x;
@@ -270,10 +308,16 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         const bool ident = (C::FPW == 1) ? nb == 0ull : ((nb >> (32 * lm.grp)) & 0xffffffffull) == 0ull;
         if ((lane & (64 / C::FPW - 1)) == 0) lds[G::MISC_OFF + my_slot] = ident ? 1 : 0;
       }
-      if constexpr (std::is_same<TW, NoTw>::value)
+      if constexpr (std::is_same<TW, NoTw>::value) {
         window_fft<N>(v, wc, fft, my_spec, twid, lm);
-      else
+      } else if constexpr (REFBITS) {
+        if (ref)
+          window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm);
+        else
+          window_fft_reg(v, wc, fft, my_spec, tw_reg, lm);
+      } else {
         window_fft_reg(v, wc, fft, my_spec, tw_reg, lm);
+      }
     }
     AVZ_STAMP(3);
     if (step + 1 < nstep) issue_loads(step + 1);
@@ -313,13 +357,16 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
             mv[3] = m4.w;
           }
           cf zm[G], zmp[G], zr[G], zrp[G];
+          uint32_t zw[G];  // REFBITS: the frame's noise word of bin column kb & 31
 #pragma unroll
           for (int i = 0; i < G; ++i) {
             if (decltype(full)::value || g0 + i < nvalid) {
               const cf* Zm = slot_ptr<N>(lds, g0 + i);
               zm[i] = Zm[kb];
               zmp[i] = Zm[kp];
-              if constexpr (MASK == MASK_IBM) {
+              if constexpr (REFBITS) {
+                zw[i] = reinterpret_cast<const uint32_t*>(slot_ptr<N>(lds, FB + g0 + i))[kb & 31];
+              } else if constexpr (MASK == MASK_IBM) {
                 const cf* Zr = slot_ptr<N>(lds, FB + g0 + i);
                 zr[i] = Zr[kb];
                 zrp[i] = Zr[kp];
@@ -345,7 +392,11 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
               }
 #if !AVZ_BINS_V1
               if constexpr (MASK == MASK_IBM) {
-                const bool noise = ibm_noise(zr[i], zrp[i]);
+                bool noise;
+                if constexpr (REFBITS)
+                  noise = (zw[i] >> (kb >> 5)) & 1u;
+                else
+                  noise = ibm_noise(zr[i], zrp[i]);
                 bits[j] |= (noise ? 1u : 0u) << (step * FB + g0 + i);
                 acc[j].add_sel(x0, x1, noise);  // weight count: popcount of bits at the end
                 if constexpr (IRM) gain[(step * FB + g0 + i) * F + kb] = irm_gain(zr[i], zrp[i]);
