@@ -138,6 +138,72 @@ __device__ __forceinline__ void transpose_addtid(cf (&v)[32], unsigned base, con
   __builtin_amdgcn_wave_barrier();
 }
 
+
+// The same planar transpose with M0 set once per plane and no lgkmcnt drain between the
+// stores and the reads (a wave's LDS operations complete in order). Timing only: on gfx950
+// ds_write_addtid_b32's M0 base is not relative to the workgroup's LDS allocation, so with
+// two blocks per CU they overwrite each other (found in the synthesis kernel: output
+// nondeterministic at 2 blocks/CU, deterministic at 1); M0[15:0] cannot reach the upper
+// 96 KB of the 160 KB LDS either.
+template <int OFF>
+__device__ __forceinline__ void addtid_store8(const float (&x)[8]) {
+  asm volatile(
+      "ds_write_addtid_b32 %0 offset:%8\n\t"
+      "ds_write_addtid_b32 %1 offset:%9\n\t"
+      "ds_write_addtid_b32 %2 offset:%10\n\t"
+      "ds_write_addtid_b32 %3 offset:%11\n\t"
+      "ds_write_addtid_b32 %4 offset:%12\n\t"
+      "ds_write_addtid_b32 %5 offset:%13\n\t"
+      "ds_write_addtid_b32 %6 offset:%14\n\t"
+      "ds_write_addtid_b32 %7 offset:%15"
+      :: "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]),
+         "i"(OFF), "i"(OFF + 264), "i"(OFF + 2 * 264), "i"(OFF + 3 * 264), "i"(OFF + 4 * 264),
+         "i"(OFF + 5 * 264), "i"(OFF + 6 * 264), "i"(OFF + 7 * 264)
+      : "memory");
+}
+__device__ __forceinline__ void transpose_addtid2(cf (&v)[32], unsigned base, const float* plane,
+                                                  int l, int g) {
+  asm volatile("s_mov_b32 m0, %0" :: "s"(base) : "m0");
+  static_for<0, 4>([&](auto q) {
+    float xr[8], xi[8];
+    static_for<0, 8>([&](auto i) { xr[i] = v[8 * q + i].x; xi[i] = v[8 * q + i].y; });
+    addtid_store8<8 * q * 264>(xr);
+    addtid_store8<8448 + 8 * q * 264>(xi);
+  });
+  __builtin_amdgcn_wave_barrier();
+  const float* re = plane + l * 66 + 32 * g;
+  const float* im = re + 2112;
+  static_for<0, 16>([&](auto q) {
+    const float2 a = *reinterpret_cast<const float2*>(re + 2 * q);
+    const float2 b = *reinterpret_cast<const float2*>(im + 2 * q);
+    v[2 * q] = {a.x, b.x};
+    v[2 * q + 1] = {a.y, b.y};
+  });
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT, 2) bench_x2_addtid2(const float* in, float* out, int iters) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 5, l = lane & 31;
+  cf* tw = reinterpret_cast<cf*>(lds + (NT / 64) * 16896);
+  Fft1024x2::fill_twiddles(tw, threadIdx.x, NT);
+  Fft1024x2 f; f.init(lane);
+  unsigned char* wbase = lds + wave * 16896;
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)wbase);
+  cf v[32];
+  static_for<0, 32>([&](auto r) { v[r] = {in[(l + 32 * r) & 1023], in[(l + 32 * r + 7) & 1023]}; });
+  __syncthreads();
+  float acc = 0;
+  for (int it = 0; it < iters; ++it) {
+    f.stage1(v, tw);
+    transpose_addtid2(v, m0, reinterpret_cast<const float*>(wbase), l, g);
+    f.stage2(v);
+  }
+  static_for<0, 32>([&](auto k) { acc += v[k].x + v[k].y; });
+  out[blockIdx.x * NT + threadIdx.x] = acc;
+}
+
 template <int NT>
 __global__ void __launch_bounds__(NT, 2) bench_x2_addtid(const float* in, float* out, int iters) {
   extern __shared__ __align__(16) unsigned char lds[];
@@ -636,6 +702,9 @@ __global__ void __launch_bounds__(512, 1) bench_x2_phase(const float* in, float*
 
 extern "C" int run_bench(int variant, const float* in, float* out, int blocks, int iters) {
   switch (variant) {
+    case 28: { auto k = bench_x2_addtid2<256>; int lds = 4 * 16896 + 8192;
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
     case 26: case 27: { auto k = variant == 26 ? bench_x2_phase<false> : bench_x2_phase<true>;
       int lds = 8 * 16896 + 8192;
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
