@@ -207,9 +207,10 @@ int avz_istft(const avz_plan* plan, int batch, int frames, const float* S, long 
               long long s_stride_f, float* out, long long out_stride, float* peak,
               void* workspace, long long workspace_bytes, void* hip_stream);
 
-/* Diagnostics: record HIP events around the kernels of every avz_mvdr_batch call on
- * this plan: enable 1 = all four (analysis, solve, synthesis, finalize), 2 = the analysis
- * kernel only (two events per call), 0 = off; enabling also resets the sums.
+/* Diagnostics: time the kernels of every avz_mvdr_batch call on this plan with HIP
+ * events carried by the kernels' own dispatches (hipExtLaunchKernel start / stop events,
+ * no marker packets between launches): enable 1 = all four (analysis, solve, synthesis,
+ * finalize), 2 = the analysis kernel only, 0 = off; enabling also resets the sums.
  * avz_plan_get_timing waits for the outstanding calls and returns the average
  * milliseconds per kernel over the calls recorded since enabling (NaN for kernels not
  * timed). Not thread-safe. */

@@ -64,8 +64,10 @@ struct avz_plan {
   Workspace ws;              // used by calls that pass no workspace (serialised by contract)
   // diagnostic per-kernel timing (avz_plan_set_timing): two event sets used alternately
   bool timing;
-  int n_ev;  // events recorded per call: 5 (all four kernels) or 2 (analysis only)
-  hipEvent_t ev[2][5];
+  int n_k;  // kernels timed per call: 4 (all) or 1 (analysis only)
+  // per kernel a (start, stop) pair carried by the kernel's own dispatch
+  // (hipExtLaunchKernel): no marker packets between the chain's launches
+  hipEvent_t ev[2][8];
   bool ev_pending[2];
   int ev_next;
   double ms_sum[4];
@@ -75,10 +77,11 @@ struct avz_plan {
 static void timing_drain(avz_plan* p, int set) {
   if (!p->ev_pending[set]) return;
   p->ev_pending[set] = false;
-  if (hipEventSynchronize(p->ev[set][p->n_ev - 1]) != hipSuccess) return;
-  for (int i = 0; i < p->n_ev - 1; ++i) {
+  if (hipEventSynchronize(p->ev[set][2 * p->n_k - 1]) != hipSuccess) return;
+  for (int i = 0; i < p->n_k; ++i) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, p->ev[set][i], p->ev[set][i + 1]) == hipSuccess) p->ms_sum[i] += ms;
+    if (hipEventElapsedTime(&ms, p->ev[set][2 * i], p->ev[set][2 * i + 1]) == hipSuccess)
+      p->ms_sum[i] += ms;
   }
   p->ms_calls += 1;
 }
@@ -86,7 +89,7 @@ static void timing_drain(avz_plan* p, int set) {
 static void timing_free(avz_plan* p) {
   if (!p->timing) return;
   for (int s = 0; s < 2; ++s)
-    for (int i = 0; i < 5; ++i) (void)hipEventDestroy(p->ev[s][i]);
+    for (int i = 0; i < 8; ++i) (void)hipEventDestroy(p->ev[s][i]);
   p->timing = false;
 }
 
@@ -325,15 +328,15 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   const int e = prepare_chain(p, a, USE_CHAIN, k);
   if (e != AVZ_OK) return e;
   avz_plan* mp = const_cast<avz_plan*>(p);  // diagnostic timing state only (not thread-safe)
-  void* evs[5];
+  void* evs[8];
   int set = -1;
   if (mp->timing) {
     set = mp->ev_next;
     mp->ev_next ^= 1;
     timing_drain(mp, set);  // the call two back: the previous call keeps the GPU busy
-    for (int i = 0; i < 5; ++i) evs[i] = mp->ev[set][i];
+    for (int i = 0; i < 8; ++i) evs[i] = mp->ev[set][i];
     k.events = evs;
-    k.n_events = mp->n_ev;
+    k.n_events = 2 * mp->n_k;
   }
   const int rc = hip_rc(avz_launch_chunked(p->cfg.n_fft, p->cfg.mask_mode, &k, stream));
   if (set >= 0 && rc == AVZ_OK) mp->ev_pending[set] = true;
@@ -468,13 +471,13 @@ extern "C" int avz_plan_set_timing(avz_plan* p, int enable) {
   for (double& m : p->ms_sum) m = 0.0;
   if (!enable) return AVZ_OK;
   if (enable != 1 && enable != 2) return AVZ_ERR_ARG;
-  p->n_ev = enable == 2 ? 2 : 5;
+  p->n_k = enable == 2 ? 1 : 4;
   for (int s = 0; s < 2; ++s)
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < 8; ++i) {
       const hipError_t e = hipEventCreateWithFlags(&p->ev[s][i], hipEventDisableSystemFence);
       if (e != hipSuccess) {
         for (int t = 0; t <= s; ++t)
-          for (int j = 0; j < (t < s ? 5 : i); ++j) (void)hipEventDestroy(p->ev[t][j]);
+          for (int j = 0; j < (t < s ? 8 : i); ++j) (void)hipEventDestroy(p->ev[t][j]);
         return hip_fail(e);
       }
     }
@@ -488,7 +491,7 @@ extern "C" int avz_plan_get_timing(avz_plan* p, double* ms_avg, int* calls) {
   timing_drain(p, p->ev_next);
   timing_drain(p, p->ev_next ^ 1);
   for (int i = 0; i < 4; ++i)
-    ms_avg[i] = i >= p->n_ev - 1 ? std::numeric_limits<double>::quiet_NaN()
+    ms_avg[i] = i >= p->n_k ? std::numeric_limits<double>::quiet_NaN()
                                  : (p->ms_calls ? p->ms_sum[i] / p->ms_calls : 0.0);
   if (calls) *calls = p->ms_calls;
   return AVZ_OK;

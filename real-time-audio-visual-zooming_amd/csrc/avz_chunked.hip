@@ -21,6 +21,7 @@
 // rt_av_zoom/core/masked_mvdr.py:50-132,
 // rt_av_zoom/core/full_audio_generating_pipeline/inference.py:88-118.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -1146,25 +1147,24 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   const dim3 pgrid((unsigned)std::min(n_items, CGeo<N>::BLOCKS * resident_cus()));
   constexpr int F = N / 2 + 1;
   const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
+  // diagnostic timing: kernel i's (start, stop) events ride on its own dispatch packet
+  // (hipExtLaunchKernel), so timing adds no marker packets between the launches
   hipEvent_t const* ev = reinterpret_cast<hipEvent_t const*>(a->events);
-  auto mark = [&](int i) {
-    if (ev && i < a->n_events) (void)hipEventRecord(ev[i], st);
-  };
+  auto evt = [&](int i) -> hipEvent_t { return (ev && i < a->n_events) ? ev[i] : nullptr; };
   const bool item_fallback = a->singular_fallback == 2 && a->beamformer == BF_MVDR;
   if (item_fallback && hipMemsetAsync(a->flag, 0, sizeof(int) * a->batch, st) != hipSuccess)
     return -3;
-  mark(0);
-  hipLaunchKernelGGL(k1, pgrid, dim3(kCThreads), lds, st, *a);
-  mark(1);
-  hipLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, *a);
-  if (item_fallback)
-    hipLaunchKernelGGL(avz_solve_fixup_kernel<N>, dim3(nsolve), dim3(kSolveThreads), 0, st, *a);
-  mark(2);
+  hipExtLaunchKernelGGL(k1, pgrid, dim3(kCThreads), lds, st, evt(0), evt(1), 0, *a);
+  if (item_fallback) {
+    hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), nullptr, 0, *a);
+    hipExtLaunchKernelGGL(avz_solve_fixup_kernel<N>, dim3(nsolve), dim3(kSolveThreads), 0, st,
+                          nullptr, evt(3), 0, *a);
+  } else {
+    hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), evt(3), 0, *a);
+  }
   const dim3 sgrid((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus()));
-  hipLaunchKernelGGL(k2, sgrid, dim3(kCThreads), lds, st, *a);
-  mark(3);
-  hipLaunchKernelGGL(k3, grid, dim3(kCThreads), 0, st, *a);
-  mark(4);
+  hipExtLaunchKernelGGL(k2, sgrid, dim3(kCThreads), lds, st, evt(4), evt(5), 0, *a);
+  hipExtLaunchKernelGGL(k3, grid, dim3(kCThreads), 0, st, evt(6), evt(7), 0, *a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

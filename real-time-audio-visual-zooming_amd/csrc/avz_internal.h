@@ -54,8 +54,8 @@ struct ChainArgs {
   int spec_frames;            // frames present in S (frames >= spec_frames read as zero)
   int cov_only;               // solve kernel: write cov_out only (the covariance stage export)
   int* flag;                  // [B] item-level (batch_mvdr) fallback flags, zeroed per call
-  void* const* events;        // host-only: 5 hipEvent_t recorded around the 4 launches, or null
-  int n_events;               // host-only: how many of them to record (5, or 2: analysis only)
+  void* const* events;        // host-only: (start, stop) hipEvent_t pairs of the 4 launches, or null
+  int n_events;               // host-only: how many of them to use (8, or 2: analysis only)
 };
 
 // Spectral-domain beamformer (avz_beamform_spectral) and the solve stage export
