@@ -215,6 +215,9 @@ int avz_istft(const avz_plan* plan, int batch, int frames, const float* S, long 
  * milliseconds per kernel over the calls recorded since enabling (NaN for kernels not
  * timed). Not thread-safe. */
 int avz_plan_set_timing(avz_plan* plan, int enable);
+/* Time one avz_mvdr_batch call in `period` (>= 1; default 1): the calls in between carry no
+ * events, so a sampled timing run costs the other calls nothing. */
+int avz_plan_set_timing_period(avz_plan* plan, int period);
 int avz_plan_get_timing(avz_plan* plan, double* ms_avg /*[4]*/, int* calls);
 
 /* Stage API: STFT of [batch][channels][x_stride] real signals into complex64

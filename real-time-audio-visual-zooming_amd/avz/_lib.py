@@ -34,6 +34,7 @@ FEAT_LOGMAG_IPD, FEAT_TFLITE = 1, 2
 EXPORTED = [
     "avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
     "avz_mvdr_batch", "avz_plan_set_timing", "avz_plan_get_timing", "avz_stft",
+    "avz_plan_set_timing_period",
     "avz_chunk_split", "avz_chunk_merge", "avz_mask_features", "avz_srp_scan",
     "avz_projection_metrics", "avz_scene_workspace_bytes", "avz_scene_mix", "avz_strerror",
     "avz_last_hip_error", "avz_version", "avz_mvdr_workspace_bytes",
@@ -129,6 +130,7 @@ def _load():
                              P, ct.c_longlong, ct.c_longlong, ct.c_longlong, P]
     I, LL = ct.c_int, ct.c_longlong
     lib.avz_plan_set_timing.argtypes = [P, I]
+    lib.avz_plan_set_timing_period.argtypes = [P, I]
     lib.avz_plan_get_timing.argtypes = [P, ct.POINTER(ct.c_double), ct.POINTER(I)]
     lib.avz_chunk_split.argtypes = [I, I, I, P, P, P, P, LL, LL, P, LL, LL, P]
     lib.avz_chunk_merge.argtypes = [I, I, I, I, P, P, P, LL, P, LL, P, I, ct.c_double, P]
@@ -150,6 +152,7 @@ def _load():
     for name in ("avz_plan_create", "avz_plan_destroy", "avz_plan_get_config", "avz_num_frames",
                  "avz_mvdr_batch", "avz_stft", "avz_chunk_split", "avz_chunk_merge",
                  "avz_plan_set_timing", "avz_plan_get_timing", "avz_mask_features",
+                 "avz_plan_set_timing_period",
                  "avz_srp_scan", "avz_projection_metrics", "avz_scene_mix",
                  "avz_scene_generate", "avz_projection_metrics_scaled", "avz_version"):
         getattr(lib, name).restype = ct.c_int

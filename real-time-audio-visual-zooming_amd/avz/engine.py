@@ -106,10 +106,12 @@ class MVDRPlan:
     # ------------------------------------------------------------------ diagnostics
     KERNELS = ("analysis", "solve", "synthesis", "finalize")
 
-    def set_timing(self, enable: bool = True, analysis_only: bool = False) -> None:
-        """Record HIP events around each of the chain's four kernels on every run()
-        (analysis_only: around the analysis kernel alone, two events per run)."""
+    def set_timing(self, enable: bool = True, analysis_only: bool = False,
+                   period: int = 1) -> None:
+        """Time each of the chain's four kernels with HIP events carried by their dispatches
+        (analysis_only: the analysis kernel alone) on one run() in `period`."""
         mode = (2 if analysis_only else 1) if enable else 0
+        check(lib.avz_plan_set_timing_period(self._h, int(period)), "avz_plan_set_timing_period")
         check(lib.avz_plan_set_timing(self._h, mode), "avz_plan_set_timing")
 
     def timing(self) -> dict:

@@ -70,6 +70,8 @@ struct avz_plan {
   hipEvent_t ev[2][8];
   bool ev_pending[2];
   int ev_next;
+  int period;      // events on one avz_mvdr_batch call in `period` (avz_plan_set_timing_period)
+  long long seen;  // calls since timing was enabled
   double ms_sum[4];
   int ms_calls;
 };
@@ -330,7 +332,7 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   avz_plan* mp = const_cast<avz_plan*>(p);  // diagnostic timing state only (not thread-safe)
   void* evs[8];
   int set = -1;
-  if (mp->timing) {
+  if (mp->timing && (mp->seen++ % mp->period) == 0) {
     set = mp->ev_next;
     mp->ev_next ^= 1;
     timing_drain(mp, set);  // the call two back: the previous call keeps the GPU busy
@@ -468,6 +470,8 @@ extern "C" int avz_plan_set_timing(avz_plan* p, int enable) {
   p->ev_pending[0] = p->ev_pending[1] = false;
   p->ev_next = 0;
   p->ms_calls = 0;
+  p->seen = 0;
+  if (p->period < 1) p->period = 1;
   for (double& m : p->ms_sum) m = 0.0;
   if (!enable) return AVZ_OK;
   if (enable != 1 && enable != 2) return AVZ_ERR_ARG;
@@ -482,6 +486,13 @@ extern "C" int avz_plan_set_timing(avz_plan* p, int enable) {
       }
     }
   p->timing = true;
+  return AVZ_OK;
+}
+
+extern "C" int avz_plan_set_timing_period(avz_plan* p, int period) {
+  if (!p || period < 1) return AVZ_ERR_ARG;
+  p->period = period;
+  p->seen = 0;
   return AVZ_OK;
 }
 

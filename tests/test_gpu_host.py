@@ -155,6 +155,11 @@ def test_plan_timing_modes(gpu_device):
             assert all(v > 0 for v in others)
         else:
             assert all(math.isnan(v) for v in others)
+    plan.set_timing(True, analysis_only=True, period=4)  # sampled: calls 0, 4, 8
+    for _ in range(9):
+        plan.run(d[0], ref_tgt=d[1], ref_int=d[2])
+    t = plan.timing()
+    assert t["calls"] == 3 and t["analysis"] > 0
     plan.set_timing(False)
     with pytest.raises(AvzError):
         plan.timing()
