@@ -1121,15 +1121,6 @@ static int resident_cus() {
   return v;
 }
 
-// Dynamic-LDS attribute of one kernel, set once (thread-safe static initialisation).
-template <auto Kern>
-static bool lds_ready(int lds) {
-  static const bool ok = hipFuncSetAttribute((const void*)Kern,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             lds) == hipSuccess;
-  return ok;
-}
-
 template <int N, int MASK, int PF>
 static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   auto k1 = avz_analysis_kernel<N, MASK, PF == PF_IRM>;

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "avz_fft.hpp"
 #include "avz_internal.h"
 
@@ -416,6 +418,25 @@ __device__ __forceinline__ void hybrid_solve_d(const double (&c)[5], int k, int 
 __device__ __forceinline__ cf apply_bin(cf alpha, cf beta, cf z, cf zp, float g) {
   const cf s = c_add(c_mul(alpha, z), c_mul(beta, c_conj(zp)));
   return {g * s.x, g * s.y};
+}
+
+
+// ---- host side
+// Dynamic-LDS attribute of one kernel, set once per device (thread-safe: the first caller
+// on a device sets it; concurrent first callers both set the same value).
+template <auto Kern>
+static bool lds_ready(int lds) {
+  static std::atomic<int> state[64];  // 0 unset, 1 set, -1 failed
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return false;
+  if (dev < 64) {
+    const int st = state[dev].load(std::memory_order_acquire);
+    if (st != 0) return st > 0;
+  }
+  const bool ok = hipFuncSetAttribute((const void*)Kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      lds) == hipSuccess;
+  if (dev < 64) state[dev].store(ok ? 1 : -1, std::memory_order_release);
+  return ok;
 }
 
 }  // namespace avz

@@ -111,13 +111,7 @@ template <int N, int FEAT>
 static int launch_stft_t(const StftArgs* a, hipStream_t st) {
   auto kern = avz_stft_kernel<N, FEAT>;
   const int lds = Geo<N, kStftThreads>::LDS_BYTES;
-  static bool attr_done = false;
-  if (!attr_done) {
-    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
-        hipSuccess)
-      return -3;
-    attr_done = true;
-  }
+  if (!lds_ready<avz_stft_kernel<N, FEAT>>(lds)) return -3;
   constexpr int NS = Geo<N, kStftThreads>::NSLOT;
   dim3 grid(a->batch, (a->max_frames + NS - 1) / NS);
   hipLaunchKernelGGL(kern, grid, dim3(kStftThreads), lds, st, *a);
