@@ -225,7 +225,10 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
   if (c >= nch) return;
-  if (c == 0 && tid == 0) A.peak_u[b] = 0u;
+  if (c == 0 && tid == 0) {
+    A.peak_u[b] = 0u;
+    if (A.peak && A.normalize != NORM_PEAK) A.peak[b] = 0.0f;  // finalize's atomicMax target
+  }
   const int t0 = c * kChunk;
   const int nframes = min(kChunk, T - t0);
   const int nstep = (nframes + FB - 1) / FB;
@@ -1068,6 +1071,32 @@ __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
   auto boundary = [&](int cc, int m) -> float {
     return (tails[(long long)(cc - 1) * H + m] + heads[(long long)cc * H + m]) * inv_wsum<N>(m);
   };
+  float* outb = A.out + (long long)b * A.out_stride;
+  if (A.normalize != NORM_PEAK) {
+    // un-normalised output (the batch driver's deferred normalisation): each chunk writes
+    // its own seam and folds its max (chunk 0: the interiors' max) into peak[b], zeroed by
+    // the analysis kernel, with an atomicMax on the float's bits (non-negative floats
+    // order as unsigned ints) — no redundant reads of the other seams
+    float pm = 0.0f;
+    if (c >= 1) {
+      const long long j = (long long)kChunk * c - 1;
+      for (int m = tid; m < H; m += NT) {
+        const float x = boundary(c, m);
+        outb[j * H + m] = x;
+        pm = fmaxf(pm, fabsf(x));
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) pm = fmaxf(pm, __shfl_xor(pm, o, 64));
+    if (lane == 0) red[wave] = pm;
+    __syncthreads();
+    if (tid == 0 && A.peak) {
+      float q = (c == 0) ? __uint_as_float(A.peak_u[b]) : 0.0f;
+#pragma unroll
+      for (int w = 0; w < NWAVE; ++w) q = fmaxf(q, red[w]);
+      atomicMax(reinterpret_cast<unsigned int*>(A.peak + b), __float_as_uint(q));
+    }
+    return;
+  }
   float pk = 0.0f;
   for (int idx = tid; idx < (nch - 1) * H; idx += NT)
     pk = fmaxf(pk, fabsf(boundary(idx / H + 1, idx % H)));
@@ -1078,13 +1107,12 @@ __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
 #pragma unroll
   for (int w = 0; w < NWAVE; ++w) pk = fmaxf(pk, red[w]);
   if (c == 0 && tid == 0 && A.peak) A.peak[b] = pk;
-  const float scale = (A.normalize == NORM_PEAK) ? 1.0f / (pk + A.norm_eps) : 1.0f;
-  float* outb = A.out + (long long)b * A.out_stride;
+  const float scale = 1.0f / (pk + A.norm_eps);
   if (c >= 1) {
     const long long j = (long long)kChunk * c - 1;
     for (int m = tid; m < H; m += NT) outb[j * H + m] = boundary(c, m) * scale;
   }
-  if (A.normalize == NORM_PEAK) {  // the chunk's interior segments 32c .. 32c+30
+  {  // the chunk's interior segments 32c .. 32c+30
     const int j0 = kChunk * c, j1 = min(kChunk * c + kChunk - 1, T - 1);
     float4* o4 = reinterpret_cast<float4*>(outb + (long long)j0 * H);
     const int n4 = (j1 - j0) * H / 4;
@@ -1270,6 +1298,9 @@ static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
   const int n_items = nch * a->batch;
   // no analysis pass in these stages: it is the analysis kernel that resets peak_u
   if (hipMemsetAsync(a->peak_u, 0, sizeof(uint32_t) * a->batch, st) != hipSuccess) return -3;
+  if (a->peak && a->normalize != NORM_PEAK &&
+      hipMemsetAsync(a->peak, 0, sizeof(float) * a->batch, st) != hipSuccess)
+    return -3;
   hipLaunchKernelGGL((avz_synthesis_kernel<N, PF, SPEC>),
                      dim3((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus())),
                      dim3(kCThreads), lds, st, *a);

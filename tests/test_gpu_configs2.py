@@ -74,9 +74,16 @@ def test_deferred_normalisation_scores_like_peak(gpu_device):
     dm, dt, di = synth.make_batch_device(Bs, start=40, n_samples=S, n_interferers=K,
                                          device=gpu_device, rng="philox")
     out_p = batch_run.gpu_enhancer(max_batch=Bs, max_samples=S, normalize="peak")(dm, dt, di)
-    out_d, peak = batch_run.gpu_enhancer(max_batch=Bs, max_samples=S)(dm, dt, di)
+    enh = batch_run.gpu_enhancer(max_batch=Bs, max_samples=S)
+    out_d, peak = enh(dm, dt, di)
     L = S
+    # peak[b] is exactly max |out[b]| (interiors and every chunk seam; seams folded in per
+    # chunk by the finalize kernel's atomicMax)
+    assert torch.equal(peak, out_d[:, :L].abs().amax(dim=1))
     assert torch.allclose(out_d[:, :L] / peak[:, None], out_p[:, :L], rtol=0, atol=1e-6)
+    # and again on the same plan: the analysis kernel resets the atomicMax target per call
+    out_d2, peak2 = enh(dm, dt, di)
+    assert torch.equal(peak2, peak) and torch.equal(out_d2, out_d)
     a = metrics.calculate_osnr_osir(out_p[:, :L], dt, di)
     b = metrics.calculate_osnr_osir(out_d[:, :L], dt, di, peak=peak)
     for x, y in zip(a, b):
