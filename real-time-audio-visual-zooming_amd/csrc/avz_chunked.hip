@@ -86,15 +86,29 @@ __device__ __forceinline__ float inv_wsum(int m) {
   return 1.0f / (wa * wa + wb * wb);
 }
 
+// Analysis window of a lane's points: register r holds sample n0 + IN_STRIDE r, weight
+// w = a0 - ac cos(2 pi IN_STRIDE r / N) + as sin(...) (angle addition on the lane's n0).
+// Registers PPL/2 apart are N/2 samples apart, where the periodic Hann window satisfies
+// w[n + N/2] = 2 a0 - w[n]: one subtraction instead of two FMAs for the upper half.
+template <int N = 1024, int PPL>
+__device__ __forceinline__ void window_apply(cf (&v)[PPL], float a0, float ac, float as) {
+  using C = KCfg<N>;
+  static_assert(C::IN_STRIDE * (PPL / 2) == N / 2, "upper-half registers are N/2 later");
+  const float a2 = a0 + a0;
+  static_for<0, PPL / 2>([&](auto r) {
+    constexpr int j = (C::IN_STRIDE * 32 / N) * r;  // 2 pi (IN_STRIDE r)/N = 2 pi j/32
+    constexpr float cr = W32::c[j % 32], sr = -W32::s[j % 32];
+    const float w = fmaf(as, sr, fmaf(-ac, cr, a0));
+    v[r] = c_scale(v[r], w);
+    v[r + PPL / 2] = c_scale(v[r + PPL / 2], a2 - w);
+  });
+}
+
 // Window + forward FFT with the lane's twiddles in registers (N = 1024 analysis).
 __device__ __forceinline__ void window_fft_reg(cf (&v)[32], const WinCoef<1024>& wc,
                                                const Fft1024x2& fft, cf* spec,
                                                const cf (&tw_reg)[31], const LaneMap<1024>& lm) {
-  static_for<0, 32>([&](auto r) {
-    constexpr float cr = W32::c[r], sr = -W32::s[r];
-    const float w = fmaf(wc.as, sr, fmaf(-wc.ac, cr, wc.a0));
-    v[r] = c_scale(v[r], w);
-  });
+  window_apply(v, wc.a0, wc.ac, wc.as);
   fft.forward_reg(v, spec, tw_reg);
   static_for<0, 32>([&](auto k) { spec[lm.out0 + 32 * k] = v[k]; });
 }
@@ -111,11 +125,7 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
                                                         const cf (&tw_reg)[31],
                                                         const LaneMap<1024>& lm) {
   constexpr int N = 1024;
-  static_for<0, 32>([&](auto r) {
-    constexpr float cr = W32::c[r], sr = -W32::s[r];
-    const float w = fmaf(wc.as, sr, fmaf(-wc.ac, cr, wc.a0));
-    v[r] = c_scale(v[r], w);
-  });
+  window_apply(v, wc.a0, wc.ac, wc.as);
   fft.forward_reg(v, spec, tw_reg);
   const int l = lm.out0;
   static_for<16, 32>([&](auto k) { spec[l + 32 * k] = v[k]; });
@@ -139,12 +149,7 @@ __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<
   opaque(a0);
   opaque(ac);
   opaque(as);
-  static_for<0, C::PPL>([&](auto r) {
-    constexpr int j = (C::IN_STRIDE * 32 / N) * r;  // 2 pi (IN_STRIDE r)/N = 2 pi j/32
-    constexpr float cr = W32::c[j % 32], sr = -W32::s[j % 32];
-    const float w = fmaf(as, sr, fmaf(-ac, cr, a0));
-    v[r] = c_scale(v[r], w);
-  });
+  window_apply<N>(v, a0, ac, as);
   fft.forward(v, spec, twid);
   static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
 }

@@ -226,8 +226,25 @@ __device__ __forceinline__ void xhalf_dit(cf (&v)[16], float sgn) {
     float ex, ox, ey, oy;
     xhalf<DIST>(v[k].x, ex, ox);
     xhalf<DIST>(v[k].y, ey, oy);
+#if AVZ_FFT_TAN
+    // tangent form: sgn W b = (sgn c)(b + t i b), |t| <= 1 (as bfly_tw)
+    constexpr int j = k;
+    if constexpr (j == 0 || j == 8) {
+      const cf t = w32mul<k>(cf{ox, oy});
+      v[k] = {fmaf(sgn, t.x, ex), fmaf(sgn, t.y, ey)};
+    } else {
+      constexpr float c = W32::c[j], s = W32::s[j];
+      constexpr bool cf_big = (c < 0 ? -c : c) >= (s < 0 ? -s : s);
+      constexpr float t = cf_big ? s / c : c / s;
+      const cf u = cf_big ? cf{fmaf(-t, oy, ox), fmaf(t, ox, oy)}
+                          : cf{fmaf(t, ox, -oy), fmaf(t, oy, ox)};
+      const float m = sgn * (cf_big ? c : s);
+      v[k] = {fmaf(m, u.x, ex), fmaf(m, u.y, ey)};
+    }
+#else
     const cf t = w32mul<k>(cf{ox, oy});
     v[k] = {fmaf(sgn, t.x, ex), fmaf(sgn, t.y, ey)};
+#endif
   });
 }
 
