@@ -99,7 +99,7 @@ struct KCfg<1024> {
   using Fft = Fft1024x2;
   static constexpr int PPL = Fft::PPL;       // complex points per lane
   static constexpr int FPW = 2;              // FFTs per wave (lane groups of 32)
-  static constexpr int GROUP_BYTES = 32 * 33 * 8;
+  static constexpr int GROUP_BYTES = Fft::GROUP_BYTES;
   static constexpr int WAVE_BYTES = 2 * GROUP_BYTES;
   static constexpr int IN_STRIDE = 32;       // sample stride between registers
   static constexpr int OUT_STRIDE = 32;      // bin/time stride between registers

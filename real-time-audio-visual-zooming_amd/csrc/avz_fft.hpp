@@ -14,7 +14,8 @@
 //  Fft1024x2 : two independent 1024-point FFTs per wave (lane group g = L>>5),
 //              32 points per lane, NO cross-lane ops: N = 32 (n1, registers) x 32 (l).
 //              step 1: 32-pt DFT in registers; twiddle W1024^{l k1} from an LDS table
-//                      [k1][l] (conflict-free); LDS transpose (32 x 33 float2 per group);
+//                      [k1][l] (conflict-free); LDS transpose (32 x 34 float2 per group:
+//                      16-B aligned rows, read back with ds_read_b128);
 //              step 2: 32-pt DFT in registers.
 //              in : lane (l = L&31, g), reg r  <->  x_g[l + 32 r]
 //              out: lane (l, g), reg k  <->  X_g[l + 32 k]
@@ -370,9 +371,18 @@ struct Fft1024 {
 };
 
 // -------------------------------------------------------------------- Fft1024x2
+#ifndef AVZ_TSTRIDE
+#define AVZ_TSTRIDE 34
+#endif
 struct Fft1024x2 {
   static constexpr int N = 1024;
   static constexpr int PPL = 32;  // points per lane
+  // Transpose row stride (complex elements). 34 keeps every row 16-B aligned, so a lane
+  // reads its row back with 16 ds_read_b128 (4 LDS cycles each, conflict-free: row l
+  // starts at bank 4 l mod 64) instead of 16 ds_read2_b64 (8 cycles each) at stride 33;
+  // the column writes are 128 contiguous bytes per 16 lanes at either stride.
+  static constexpr int TS = AVZ_TSTRIDE;
+  static constexpr int GROUP_BYTES = 32 * TS * 8;
   int l;
 
   __device__ __forceinline__ void init(int lane) { l = lane & 31; }
@@ -423,9 +433,18 @@ struct Fft1024x2 {
     stage2(v);
   }
   __device__ __forceinline__ void transpose(cf (&v)[32], cf* scratch) const {
-    static_for<0, 32>([&](auto k) { scratch[k * 33 + l] = v[k]; });
+    static_for<0, 32>([&](auto k) { scratch[k * TS + l] = v[k]; });
     __builtin_amdgcn_wave_barrier();
-    static_for<0, 32>([&](auto r) { v[r] = scratch[l * 33 + r]; });
+    if constexpr (TS % 2 == 0) {
+      const float4* row = reinterpret_cast<const float4*>(scratch + l * TS);
+      static_for<0, 16>([&](auto q) {
+        const float4 x = row[q];
+        v[2 * q] = cf{x.x, x.y};
+        v[2 * q + 1] = cf{x.z, x.w};
+      });
+    } else {
+      static_for<0, 32>([&](auto r) { v[r] = scratch[l * TS + r]; });
+    }
     __builtin_amdgcn_wave_barrier();
   }
   __device__ __forceinline__ void stage2(cf (&v)[32]) const { dft32(v); }

@@ -2,6 +2,8 @@
 // LDS transpose -> natural-order spectrum store -> block barrier} ITERS times.
 // Reports nothing itself; time it from Python (tools/micro/fftbench.py).
 #include <hip/hip_runtime.h>
+// the variants below size their LDS for the stride-33 transpose (8448-B groups)
+#define AVZ_TSTRIDE 33
 #include "../../real-time-audio-visual-zooming_amd/csrc/avz_common.hpp"
 using namespace avz;
 
