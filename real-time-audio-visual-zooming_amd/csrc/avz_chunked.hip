@@ -828,10 +828,10 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       for (int p = 0; p < NPAIR; ++p) {
         const cf* Za = slot_ptr<N>(lds, 2 * p);
         const cf* Zb = slot_ptr<N>(lds, 2 * p + 1);
-        za[p] = Za[kb];
-        zap[p] = Za[kp];
-        zb[p] = Zb[kb];
-        zbp[p] = Zb[kp];
+        za[p] = lds_read(Za + kb);
+        zap[p] = lds_read(Za + kp);
+        zb[p] = lds_read(Zb + kb);
+        zbp[p] = lds_read(Zb + kp);
       }
       // External mask with t-contiguous, 16-B aligned rows (the U-Net / TFLite outputs):
       // the bin's FB gains of this step in FB/4 16-B loads instead of FB scattered ones.
@@ -968,7 +968,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       // output register k of lane (l, h) is sample l + 512 h + 32 k)
       cf u[16];
       cf* Zi = slot_ptr<N>(lds, 2 * wave);
-      static_for<0, 16>([&](auto r) { u[r] = c_conj(Zi[64 * r + lane]); });
+      static_for<0, 16>([&](auto r) { u[r] = c_conj(lds_read(Zi + 64 * r + lane)); });
       Fft1024::forward_tw(u, Zi, twid, lane);
       float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * wave + 1));
       const int n0 = (lane & 31) + 512 * (lane >> 5);
