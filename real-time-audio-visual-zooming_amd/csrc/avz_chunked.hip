@@ -39,6 +39,10 @@
 
 namespace avz {
 
+#ifndef AVZ_SYN_INV2
+#define AVZ_SYN_INV2 1
+#endif
+
 constexpr int kChunk = 32;      // frames per chunk = bits of one mask word
 constexpr int kCThreads = 256;  // 4 waves
 
@@ -688,6 +692,8 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   constexpr int NSG = NT / M4;        // segment groups
   constexpr int SPT = FB / NSG;       // segments per thread per step
   static_assert(SPT * NSG == FB, "OLA mapping");
+  // N = 1024 inverse as two x2 transforms on waves 0-1 instead of four 64-lane x1 ones
+  constexpr bool INV2 = N == 1024 && !AVZ_X1 && AVZ_SYN_INV2;
 
   cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
   float* red = reinterpret_cast<float*>(lds + G::MISC_OFF);
@@ -788,7 +794,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);  // previous frame's second half (sgrp 0)
   float* outb = A.out + (long long)b * A.out_stride;
   float peak = 0.0f;
-  const bool ifft_wave = wave < NPAIR / C::FPW;  // N = 512: waves holding a pair
+  const bool ifft_wave = wave < NPAIR / C::FPW;  // waves holding a pair (x2 inverse)
   float wi_c = 0.f, wi_s = 0.f;  // N = 1024 inverse: 0.25 cos / sin(2 pi n0 / N), x1 layout
   if constexpr (N == 1024) {
     double sn, cs;
@@ -808,9 +814,11 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
 #endif
     if constexpr (!SPEC) {
       window_fft<N>(v, wc, fft, my_spec, twid, lm);
-      // x2: the next step's loads fly through apply, inverse FFT and OLA; x1 issues them
-      // after the inverse FFT (its registers are needed there at four waves per SIMD)
-      if (!AVZ_X1 && more) issue_loads(step + 1);
+      // x2 with the x1 inverse: the next step's loads fly through apply, inverse FFT and
+      // OLA. x1 and the two-wave x2 inverse issue them after the inverse FFT, whose
+      // registers they are (measured: issuing them here on the two pairless waves, or
+      // after the overlap-add, costs 1-3 us)
+      if (!AVZ_X1 && !INV2 && more) issue_loads(step + 1);
     }
     lds_barrier();
     AVZ_STAMP(6);
@@ -963,7 +971,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
           Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
         });
       }
-    } else if constexpr (N == 1024) {
+    } else if constexpr (N == 1024 && !INV2) {
       // four pairs, four waves: one 64-lane 1024-point transform each (x1 layout:
       // output register k of lane (l, h) is sample l + 512 h + 32 k)
       cf u[16];
@@ -980,21 +988,31 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
       });
     } else if (ifft_wave) {
+      // N = 512, and N = 1024 with AVZ_SYN_INV2: one packed pair per lane group, two
+      // transforms per wave on the waves holding pairs (the 1024-point x2 form runs in the
+      // sample registers v, so the next step's loads wait until it is done)
       const int p = wave * C::FPW + lm.grp;
       cf* Zi = slot_ptr<N>(lds, 2 * p);
-      cf u[PPL];
-      static_for<0, PPL>([&](auto r) { u[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
-      fft.forward(u, Zi, twid);
-      float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
-      static_for<0, PPL>([&](auto k) {
-        constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
-        const float w = fmaf(wc.ss, sk, fmaf(-wc.sc, ck, wc.s0));
-        const int n = lm.out0 + C::OUT_STRIDE * k;
-        Cp[n] = u[k].x * w;       // frame 2p   (real part of the inverse)
-        Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
-      });
+      auto inverse = [&](cf (&u)[PPL]) {
+        static_for<0, PPL>([&](auto r) { u[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
+        fft.forward(u, Zi, twid);
+        float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
+        static_for<0, PPL>([&](auto k) {
+          constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+          const float w = fmaf(wc.ss, sk, fmaf(-wc.sc, ck, wc.s0));
+          const int n = lm.out0 + C::OUT_STRIDE * k;
+          Cp[n] = u[k].x * w;       // frame 2p   (real part of the inverse)
+          Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
+        });
+      };
+      if constexpr (INV2) {
+        inverse(v);
+      } else {
+        cf u[PPL];
+        inverse(u);
+      }
     }
-    if (AVZ_X1 && more) issue_loads(step + 1);
+    if ((AVZ_X1 || INV2) && !SPEC && more) issue_loads(step + 1);
     lds_barrier();
     AVZ_STAMP(8);
 
