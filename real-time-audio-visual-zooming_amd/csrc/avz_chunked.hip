@@ -158,6 +158,48 @@ __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<
   static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
 }
 
+#ifndef AVZ_SHARE_LOADS
+#define AVZ_SHARE_LOADS 1
+#endif
+// Shared-half loads of a wave's frame pair (Fft1024x2, N = 1024): frames 2w and 2w + 1
+// overlap by N/2 = 16 registers, so the wave loads 1536 samples per stream (24 loads)
+// instead of 2 x 1024 (32). Lane group 1 holds its frame rotated by N/2 — register r < 16
+// is sample 512 + 32 r + l of the frame, r >= 16 is sample 32 (r - 16) + l, i.e. the
+// second half of frame 2w — so both groups take the shared half in the same registers:
+//   v[j], j < 16:   group 0 samples sp + 32 j, group 1 sp + 1024 + 32 j (own halves);
+//   v[16 + 2 i]:    group 0 sample sp + 512 + 64 i, group 1 the next 32 (shared half),
+//                   spread to v[16 + 2 i] / v[17 + 2 i] on every lane by one
+//                   v_permlane32_swap per float once the loads have landed (pair_finish).
+// sp = the pair's first sample + l. The rotation is a circular shift by N/2 of group 1's
+// frame: its window weights swap halves (ac, as negated: window_apply's w <-> 2 a0 - w)
+// and its spectrum comes out as (-1)^k X[k], undone by (-1)^k1 folded into the stage-1
+// twiddles. Analysis kernel only: in the synthesis kernel (LDS twiddles, the sign folded
+// into the odd frames' post-filter gain) it measured 73.1 -> 75.1 us against the analysis
+// kernel's 80.3 -> 79.0 (profiles/r02z/ab_experiments.txt).
+template <bool NONNEG>
+__device__ __forceinline__ void pair_loads(cf (&v)[32], rsrc_t r0, rsrc_t r1, int sp, int g) {
+  static_for<0, 16>([&](auto j) {
+    const int e = sp + 1024 * g + 32 * j;
+    v[j].x = NONNEG ? bload_nn(r0, e) : bload(r0, e);
+    v[j].y = NONNEG ? bload_nn(r1, e) : bload(r1, e);
+  });
+  static_for<0, 8>([&](auto i) {
+    const int e = sp + 512 + 32 * (2 * i) + 32 * g;
+    v[16 + 2 * i].x = NONNEG ? bload_nn(r0, e) : bload(r0, e);
+    v[16 + 2 * i].y = NONNEG ? bload_nn(r1, e) : bload(r1, e);
+  });
+}
+__device__ __forceinline__ void pair_finish(cf (&v)[32]) {
+  static_for<0, 8>([&](auto i) {
+    const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[16 + 2 * i].x),
+                                                     __float_as_uint(v[16 + 2 * i].x), false, false);
+    const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[16 + 2 * i].y),
+                                                     __float_as_uint(v[16 + 2 * i].y), false, false);
+    v[16 + 2 * i] = cf{__uint_as_float(rx[0]), __uint_as_float(ry[0])};
+    v[17 + 2 * i] = cf{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+  });
+}
+
 // Samples of utterance b: the device length clamped to the host-validated max_len (so an
 // inconsistent len[] never moves an access outside the caller's rows), or max_len for all.
 __device__ __forceinline__ int utt_len(const ChainArgs& A, int b) {
@@ -224,6 +266,11 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   // (window_fft_reg_ibm_bits) instead of the whole reference spectrum
   constexpr bool REFBITS = AVZ_REFBITS && !AVZ_BINS_V1 && N == 1024 && MASK == MASK_IBM && !IRM &&
                            !std::is_same<TW, NoTw>::value;
+  // shared-half frame-pair loads (pair_loads); needs the twiddle signs of the register path
+  // (not IPD: its decisions are pinned bit-exact to the reference's, and the rotated
+  // transform's rounding moved one of 1.3e5 on the ipd_test golden)
+  constexpr bool SHARE = AVZ_SHARE_LOADS && N == 1024 && MASK != MASK_IPD &&
+                         !std::is_same<TW, NoTw>::value;
 
   cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
   const int tid = threadIdx.x;
@@ -248,6 +295,10 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   lm.init(lane);
   WinCoef<N> wc;
   wc.init(lm);
+  if (SHARE && lm.grp) {  // rotated frame: window halves swapped
+    wc.ac = -wc.ac;
+    wc.as = -wc.as;
+  }
   const int my_slot = wave * C::FPW + lm.grp;
   cf* my_spec = slot_ptr<N>(lds, my_slot);
   // IBM: waves 0-1 transform the mic pair, waves 2-3 the reference pair (wave-uniform)
@@ -265,6 +316,14 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   }
   cf v[PPL];
   auto issue_loads = [&](int step) {
+    if constexpr (SHARE) {
+      const int sp = (t0 + step * FB + wave_frame0) * H - N / 2 + lm.in0;
+      if (t0 + step * FB + wave_frame0 >= 1)
+        pair_loads<true>(v, r_re, r_im, sp, lm.grp);
+      else
+        pair_loads<false>(v, r_re, r_im, sp, lm.grp);
+      return;
+    }
     const int s0 = (t0 + step * FB + my_frame) * H - N / 2 + lm.in0;
     if (t0 + step * FB + wave_frame0 >= 1) {  // wave-uniform: no negative sample index
       static_for<0, PPL>([&](auto r) {
@@ -309,6 +368,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     AVZ_STAMP(0);
 #endif
     if (live) {
+      if constexpr (SHARE) pair_finish(v);
       if constexpr (MASK == MASK_IPD) {
         // Bitwise-identical channel samples give bitwise-identical pocketfft spectra in the
         // reference, hence equal angles (weight 0.01) in every bin of the frame; the packed
@@ -541,6 +601,9 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysi
     Fft1024x2 f;
     f.init(threadIdx.x & 63);
     f.load_twiddles(tw_reg, reinterpret_cast<const cf*>(lds + G::TW_OFF));
+    if (AVZ_SHARE_LOADS && MASK != MASK_IPD && (threadIdx.x & 32)) {  // rotated frames: (-1)^k1 (pair_loads)
+      static_for<0, 16>([&](auto i) { tw_reg[2 * i] = cf{-tw_reg[2 * i].x, -tw_reg[2 * i].y}; });
+    }
     for (int it = blockIdx.x; it < n_items; it += gridDim.x)
       analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, tw_reg);
   } else {
