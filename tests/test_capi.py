@@ -69,3 +69,25 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
         assert int(got[cname]) == ct.sizeof(cls)
         for f, _ in cls._fields_:
             assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
+
+
+def test_integration_shim_structs_match_the_host_layer():
+    """The reference-side ctypes shim printed in INTEGRATION.md declares the same struct
+    fields (names and C types, in order) as avz._lib, which the header-layout test above
+    pins to include/avz.h: a stale shim would hand the library a short struct."""
+    import ast
+    import textwrap
+    from avz import _lib
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```python\n(.*?)```", text, re.S)
+    shim = {}
+    for b in blocks:
+        for node in ast.walk(ast.parse(textwrap.dedent(b))):
+            if isinstance(node, ast.ClassDef):
+                for st in node.body:
+                    if isinstance(st, ast.Assign) and st.targets[0].id == "_fields_":
+                        shim[node.name] = eval(compile(ast.Expression(st.value), "shim", "eval"),
+                                               {"ct": ct})
+    assert {"AvzConfig", "AvzBatchArgs", "AvzSpectralArgs"} <= set(shim)
+    for name, fields in shim.items():
+        assert fields == list(getattr(_lib, name)._fields_), name
