@@ -1183,7 +1183,22 @@ __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
     }
     return;
   }
+  // The chunk's interior segments 32c .. 32c+30 are read into registers first: their loads
+  // do not depend on the utterance peak, so they stream while the seam maxima below are
+  // fetched (all blocks are resident at once; reading them after the peak left every
+  // block waiting on its seam loads before any bulk traffic started).
+  constexpr int U = ((kChunk - 1) * H / 4 + NT - 1) / NT;
+  const int j0 = kChunk * c, j1 = min(kChunk * c + kChunk - 1, T - 1);
+  float4* o4 = reinterpret_cast<float4*>(outb + (long long)j0 * H);
+  const int n4 = (j1 - j0) * H / 4;
+  float4 xin[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = tid + u * NT;
+    if (i < n4) xin[u] = o4[i];
+  }
   float pk = 0.0f;
+#pragma unroll 4
   for (int idx = tid; idx < (nch - 1) * H; idx += NT)
     pk = fmaxf(pk, fabsf(boundary(idx / H + 1, idx % H)));
   for (int o = 32; o > 0; o >>= 1) pk = fmaxf(pk, __shfl_xor(pk, o, 64));
@@ -1198,12 +1213,11 @@ __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
     const long long j = (long long)kChunk * c - 1;
     for (int m = tid; m < H; m += NT) outb[j * H + m] = boundary(c, m) * scale;
   }
-  {  // the chunk's interior segments 32c .. 32c+30
-    const int j0 = kChunk * c, j1 = min(kChunk * c + kChunk - 1, T - 1);
-    float4* o4 = reinterpret_cast<float4*>(outb + (long long)j0 * H);
-    const int n4 = (j1 - j0) * H / 4;
-    for (int i = tid; i < n4; i += NT) {
-      float4 x = o4[i];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = tid + u * NT;
+    if (i < n4) {
+      float4 x = xin[u];
       x.x *= scale; x.y *= scale; x.z *= scale; x.w *= scale;
       o4[i] = x;
     }
