@@ -1230,6 +1230,20 @@ using namespace avz;
 
 extern "C" int avz_chunk_frames(void) { return kChunk; }
 
+static int resident_cus();
+
+// The synthesis launch of the chain and of the stage exports (persistent grid).
+template <int N, int PF>
+static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  const int nch = (a->max_frames + kChunk - 1) / kChunk;
+  constexpr int lds = CGeo<N>::LDS_BYTES;
+  if (!lds_ready<avz_synthesis_kernel<N, PF>>(lds)) return -3;
+  const int n_items = nch * a->batch;
+  const dim3 sgrid((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus()));
+  hipExtLaunchKernelGGL(avz_synthesis_kernel<N, PF>, sgrid, dim3(kCThreads), lds, st, e0, e1, 0, *a);
+  return 0;
+}
+
 #ifdef AVZ_STAMPS
 extern "C" int avz_debug_set_stamps_chunked(void* dev_ptr) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -3;
@@ -1252,13 +1266,10 @@ static int resident_cus() {
 template <int N, int MASK, int PF>
 static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   auto k1 = avz_analysis_kernel<N, MASK, PF == PF_IRM>;
-  auto k2 = avz_synthesis_kernel<N, PF>;
   auto k3 = avz_finalize_kernel<N>;
   auto ks = avz_solve_kernel<N>;
   constexpr int lds = CGeo<N>::LDS_BYTES;
-  if (!lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM>>(lds) ||
-      !lds_ready<avz_synthesis_kernel<N, PF>>(lds))
-    return -3;
+  if (!lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM>>(lds)) return -3;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
   const dim3 grid(nch, a->batch);
@@ -1281,8 +1292,7 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   } else {
     hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), evt(3), 0, *a);
   }
-  const dim3 sgrid((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus()));
-  hipExtLaunchKernelGGL(k2, sgrid, dim3(kCThreads), lds, st, evt(4), evt(5), 0, *a);
+  if (launch_synthesis<N, PF>(a, st, evt(4), evt(5)) != 0) return -3;
   hipExtLaunchKernelGGL(k3, grid, dim3(kCThreads), 0, st, evt(6), evt(7), 0, *a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
@@ -1392,7 +1402,7 @@ extern "C" int avz_launch_covariance(int n_fft, int mask_mode, const ChainArgs* 
 template <int N, int PF, bool SPEC>
 static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
   constexpr int lds = CGeo<N>::LDS_BYTES;
-  if (!lds_ready<avz_synthesis_kernel<N, PF, SPEC>>(lds)) return -3;
+  if (SPEC && !lds_ready<avz_synthesis_kernel<N, PF, SPEC>>(lds)) return -3;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
   const int n_items = nch * a->batch;
@@ -1401,9 +1411,13 @@ static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
   if (a->peak && a->normalize != NORM_PEAK &&
       hipMemsetAsync(a->peak, 0, sizeof(float) * a->batch, st) != hipSuccess)
     return -3;
-  hipLaunchKernelGGL((avz_synthesis_kernel<N, PF, SPEC>),
-                     dim3((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus())),
-                     dim3(kCThreads), lds, st, *a);
+  if constexpr (SPEC) {
+    hipLaunchKernelGGL((avz_synthesis_kernel<N, PF, SPEC>),
+                       dim3((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus())),
+                       dim3(kCThreads), lds, st, *a);
+  } else {
+    if (launch_synthesis<N, PF>(a, st, nullptr, nullptr) != 0) return -3;
+  }
   hipLaunchKernelGGL(avz_finalize_kernel<N>, dim3(nch, a->batch), dim3(kCThreads), 0, st, *a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -5,6 +5,7 @@
 // the variants below size their LDS for the stride-33 transpose (8448-B groups)
 #define AVZ_TSTRIDE 33
 #include "../../real-time-audio-visual-zooming_amd/csrc/avz_common.hpp"
+#include "reg_transpose.hpp"
 using namespace avz;
 
 template <int NT>
@@ -75,6 +76,10 @@ __global__ void __launch_bounds__(NT, 2) bench_x2m(const float* in, float* out, 
       dft32(v);
       __builtin_amdgcn_sched_barrier(0);
       dft32(v);
+    } else if constexpr (MODE == 5) {  // register (DPP / permlane16) transpose
+      f.stage1(v, tw);
+      transpose32_regs(v, l);
+      f.stage2(v);
     } else {
       f.forward(v, scr, tw);
     }
@@ -755,7 +760,7 @@ extern "C" int run_bench(int variant, const float* in, float* out, int blocks, i
       int lds = 4 * 16896 + 8192;
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }
-    case 4: case 5: case 6: case 7: case 8: { auto k = variant == 4 ? bench_x2m<256, 0> : variant == 5 ? bench_x2m<256, 1> : variant == 6 ? bench_x2m<256, 2> : variant == 7 ? bench_x2m<256, 3> : bench_x2m<256, 4>;
+    case 4: case 5: case 6: case 7: case 8: case 29: { auto k = variant == 4 ? bench_x2m<256, 0> : variant == 5 ? bench_x2m<256, 1> : variant == 6 ? bench_x2m<256, 2> : variant == 7 ? bench_x2m<256, 3> : variant == 29 ? bench_x2m<256, 5> : bench_x2m<256, 4>;
       int lds = 4 * 16896 + 8192;
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, in, out, iters); break; }

@@ -26,8 +26,9 @@ names = {0: "x2 (32 pts/lane), 8 waves/block", 1: "x1 (16 pts/lane), 16 waves/bl
          23: "p3 FFT only (16 pts/lane, 2 transposes), 4 w/b x4", 24: "p3 + wave-local spectrum round trip",
          25: "x1 FFT only (permlane32), 4 w/b x4",
          26: "x2 FFT only, 8 w/b, waves in phase", 27: "x2 FFT only, 8 w/b, SIMD pairs half an FFT apart",
-         28: "x2 FFT only, addtid planar transpose, no drain"}
-ffts_per_block = {28: 8, 26: 16, 27: 16, 23: 4, 24: 4, 25: 4, 0: 16, 1: 16, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 8, 9: 8, 10: 8, 11: 8, 12: 8, 13: 8, 14: 8, 15: 8, 16: 8, 17: 8, 18: 8, 19: 8, 20: 8, 21: 8, 22: 8}
+         28: "x2 FFT only, addtid planar transpose, no drain",
+         29: "x2 FFT only, register (DPP) transpose"}
+ffts_per_block = {29: 8, 28: 8, 26: 16, 27: 16, 23: 4, 24: 4, 25: 4, 0: 16, 1: 16, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 8, 9: 8, 10: 8, 11: 8, 12: 8, 13: 8, 14: 8, 15: 8, 16: 8, 17: 8, 18: 8, 19: 8, 20: 8, 21: 8, 22: 8}
 import sys
 VARS = [(int(a.split(':')[0]), int(a.split(':')[1])) for a in sys.argv[1:]] or [(4, 512), (23, 1024), (24, 1024), (25, 1024)]
 for v, blocks in VARS:
