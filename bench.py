@@ -6,11 +6,19 @@ batch of B = 256 synthetic 2-mic utterances of 4.0 s (64000 samples @ 16 kHz),
 TF-bins per utterance. One step = one avz_mvdr_batch call over the whole batch: the
 analysis (STFT -> IBM -> masked covariance partials), solve (fp64 MVDR), synthesis
 (STFT -> apply + IBM post-filter -> iSTFT/OLA) and finalize (chunk seams, peak
-normalisation) kernels, inputs resident in HBM. Per-kernel times come from HIP events
-the plan records around each launch on the launch stream (avz_plan_set_timing).
+normalisation) kernels, inputs resident in HBM. The timed steps alternate between two
+distinct batches (2 x 262 MB of input, more than the 256 MB Infinity Cache), so no step
+re-reads the previous step's input from the die. Per-kernel times come from HIP events the
+plan records around each launch on the launch stream (avz_plan_set_timing).
 Multi-GPU: one process per GPU, utterances sharded (weak scaling, no data-path
 collective); the only collectives are the final RCCL all-reduce of the SIR metric sums
-and the max-over-ranks step time.
+and the max-over-ranks step time. With --gpus N > 1 the per-GPU shard defaults to
+configs[2]'s (B = 4096 over 8 GPUs = 512 utterances per GPU, 3 interferers).
+
+The N = 1 default run also measures, in the same JSON line (`secondary`), every other
+single-GPU configuration the same way: configs[2]'s per-GPU shard, configs[3] (IPD,
+B = 1024), oracle_debug's 512/256 STFT, the batch driver's deferred normalisation and
+configs[4]'s MVDR chain (4096 two-second external-mask items).
 
 Other workloads (parity configs, measured on request, same JSON line):
   --workload ipd   configs[3]: heuristic IPD mask (masked_mvdr.py), B = 1024, no
@@ -42,9 +50,10 @@ for _p in (ROOT, PKG):
 import numpy as np  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
-N_FFT, HOP, FS, SECONDS = 1024, 512, 16000, 4.0
+FS, SECONDS = 16000, 4.0
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 DEFAULT_BATCH = {"ibm": 256, "ipd": 1024, "unet": 1024}
+CPU_SHARE = 16  # host cores per GPU on the MI355X boxes (their CPU share; nproc shows the machine)
 WORKLOAD_TEXT = {
     "ibm": "configs[1]: B={B} utterances/GPU, {k} interferers, oracle IBM, {n}-pt STFT hop {h} "
            "@16 kHz, 4.0 s utterances",
@@ -52,6 +61,9 @@ WORKLOAD_TEXT = {
            "interferers, {n}-pt STFT hop {h} @16 kHz, 4.0 s utterances",
     "unet": "configs[4]: B={B} utterances/GPU -> 2-s chunks, U-Net mask (PyTorch-ROCm {unet_dtype}, "
             "random init) -> external-mask MVDR, {n}-pt STFT hop {h}, chunk OLA",
+    "chain4": "configs[4] MVDR chain only: B={B} utterances/GPU -> 2-s chunk items, external "
+              "target mask (a fixed synthetic mask stands in for the U-Net output) -> MVDR, "
+              "max(M, 0.05) post-filter, iSTFT, {n}-pt STFT hop {h}",
 }
 
 
@@ -61,12 +73,19 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(DEFAULT_BATCH), default="ibm")
-    ap.add_argument("--batch", type=int, default=0, help="utterances per GPU (0: workload default)")
-    ap.add_argument("--interferers", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=0,
+                    help="utterances per GPU (0: workload default; ibm at N > 1: 512, configs[2])")
+    ap.add_argument("--interferers", type=int, default=0,
+                    help="interferers per scene (0: 2; ibm at N > 1: 3, configs[2])")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="time box of the CPU baseline workers")
-    ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, available cores)")
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help=f"0: min({CPU_SHARE}, available cores) -- the box's CPU share per GPU")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="N = 1: skip the secondary configurations")
+    ap.add_argument("--single-batch", action="store_true",
+                    help="time one batch over and over instead of alternating two")
     ap.add_argument("--n-fft", type=int, choices=(512, 1024), default=1024,
                     help="STFT size (hop n/2); 1024 is the BASELINE configs, 512 oracle_debug's default")
     ap.add_argument("--unet-dtype", choices=("fp32", "bf16"), default="fp32",
@@ -85,7 +104,9 @@ def parse():
     ap.add_argument("--no-settle", action="store_true",
                     help="skip the clock-settling steps before the warmup (cold-GPU timing)")
     a = ap.parse_args()
-    a.batch = a.batch or DEFAULT_BATCH[a.workload]
+    shard2 = a.workload == "ibm" and a.gpus > 1
+    a.batch = a.batch or (512 if shard2 else DEFAULT_BATCH[a.workload])
+    a.interferers = a.interferers or (3 if shard2 else 2)
     return a
 
 
@@ -94,11 +115,12 @@ _CPU_SAMPLE = None
 
 
 def _cpu_worker(args):
-    wid, budget, workload, vectorised = args
+    wid, budget, workload, vectorised, n_fft = args
     from threadpoolctl import threadpool_limits
 
     from oracle import avz_oracle as O
     mix, tgt, itf = _CPU_SAMPLE
+    hop = n_fft // 2
     n = 0
     bins = 0
     t0 = time.perf_counter()
@@ -106,17 +128,17 @@ def _cpu_worker(args):
         while time.perf_counter() - t0 < budget:
             b = (wid + n) % mix.shape[0]
             if workload == "ipd":
-                O.masked_mvdr_vec(mix[b], n_fft=N_FFT, hop=HOP)
+                O.masked_mvdr_vec(mix[b], n_fft=n_fft, hop=hop)
             elif vectorised:
-                O.oracle_debug_vec(mix[b], tgt[b], itf[b], n_fft=N_FFT, hop=HOP, sigma=1.0)
+                O.oracle_debug_vec(mix[b], tgt[b], itf[b], n_fft=n_fft, hop=hop, sigma=1.0)
             else:
-                O.oracle_debug_loop(mix[b], tgt[b], itf[b], n_fft=N_FFT, hop=HOP, sigma=1.0)
-            bins += (N_FFT // 2 + 1) * O.n_frames(mix.shape[-1], N_FFT, HOP)
+                O.oracle_debug_loop(mix[b], tgt[b], itf[b], n_fft=n_fft, hop=hop, sigma=1.0)
+            bins += (n_fft // 2 + 1) * O.n_frames(mix.shape[-1], n_fft, hop)
             n += 1
     return n, bins, time.perf_counter() - t0
 
 
-def cpu_baseline(sample, seconds, workers, workload):
+def cpu_baseline(sample, seconds, workers, workload, n_fft, available):
     """The oracle restatement of the same path (oracle/avz_oracle.py, kind 'port') on the
     host cores, time-boxed, one single-threaded worker process per core: the
     loop-faithful oracle_debug (ibm) or the vectorised masked_mvdr (ipd)."""
@@ -126,12 +148,12 @@ def cpu_baseline(sample, seconds, workers, workload):
     ctx = mp.get_context("fork")  # forked before any GPU initialisation
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
-        res = pool.map(_cpu_worker, [(w, seconds, workload, False) for w in range(workers)])
+        res = pool.map(_cpu_worker, [(w, seconds, workload, False, n_fft) for w in range(workers)])
         wall = time.perf_counter() - t0
         # the vectorised restatement is reported beside the loop-faithful one
         vec = None
         if workload == "ibm":
-            rv = pool.map(_cpu_worker, [(w, seconds / 2, workload, True) for w in range(workers)])
+            rv = pool.map(_cpu_worker, [(w, seconds / 2, workload, True, n_fft) for w in range(workers)])
             vec = sum(r[1] for r in rv) / max(r[2] for r in rv)
     utts = sum(r[0] for r in res)
     bins = sum(r[1] for r in res)
@@ -139,10 +161,12 @@ def cpu_baseline(sample, seconds, workers, workload):
             if workload == "ipd" else
             "loop-faithful restatement of oracle_debug.main (oracle IBM, sigma 1)")
     return {"value": bins / max(r[2] for r in res), "unit": "TF-bins/s", "cores": workers,
-            "kind": "port", "value_vectorised": vec,
+            "cores_available": available, "kind": "port", "value_vectorised": vec,
             "sample": (f"time-boxed {seconds:.0f} s x {workers} single-threaded workers over "
                        f"{sample[0].shape[0]} distinct utterances of the same workload (4.0 s, "
-                       f"{N_FFT}/{HOP}): {utts} utterances; {what} minus WAV I/O; wall {wall:.1f} s"
+                       f"{n_fft}/{n_fft // 2}): {utts} utterances; {what} minus WAV I/O; wall "
+                       f"{wall:.1f} s; {workers} of the {available} cores the process may run "
+                       f"on: the box's CPU share per GPU is {CPU_SHARE}"
                        + ("; value_vectorised: the vectorised restatement (oracle_debug_vec), "
                           "same workers, half the time box" if vec is not None else ""))}
 
@@ -154,131 +178,144 @@ SETTLE_MIN_S = 0.1  # sustained load before the convergence test (the clock ramp
 SETTLE_MAX_S = 0.6  # cap on the settling phase
 
 
-def setup_chain(args, B, S, dev, d_mix, d_tgt, d_itf):
-    """ibm / ipd: one avz_mvdr_batch call per step (inputs already resident in HBM)."""
+def bytes_per_bin(workload, n_fft):
+    """every 4-byte sample stream costs 4 H / F B per TF-bin (3.992 at
+    1024/512). ibm: 2 mic + 2 references + output = 19.96 B/bin; ipd: 2 mic + output =
+    11.98; external mask: + 4 B/bin of mask = 15.98."""
+    per_stream = 4.0 * (n_fft // 2) / (n_fft // 2 + 1)
+    return {"ibm": 5 * per_stream, "ipd": 3 * per_stream,
+            "unet": 3 * per_stream + 4.0, "chain4": 3 * per_stream + 4.0}[workload]
+
+
+def gen_batch(spec, dev, start, scenes):
+    import torch
+
+    from avz import synth
+    S = int(SECONDS * FS)
+    if scenes == "philox":
+        return synth.make_batch_device(spec["B"], start=start, n_samples=S,
+                                       n_interferers=spec["k"], device=dev, rng="philox")
+    hm, ht, hi = synth.make_batch(spec["B"], start=start, n_samples=S, n_interferers=spec["k"])
+    return tuple(torch.from_numpy(a).to(dev) for a in (hm, ht, hi))
+
+
+def setup_chain(spec, dev, batches):
+    """ibm / ipd: one avz_mvdr_batch call per step (inputs already resident in HBM), the
+    steps alternating over the batches."""
     import torch
 
     import avz
-    norm = "peak" if args.normalize == "peak" else "none"
-    if args.workload == "ibm":
-        plan = avz.MVDRPlan(n_fft=N_FFT, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
+    B, n_fft, S = spec["B"], spec["n_fft"], int(SECONDS * FS)
+    hop = n_fft // 2
+    norm = "peak" if spec["normalize"] == "peak" else "none"
+    if spec["workload"] == "ibm":
+        plan = avz.MVDRPlan(n_fft=n_fft, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
                             normalize=norm, max_batch=B, max_samples=S)
         streams = 4
     else:
-        plan = avz.MVDRPlan(n_fft=N_FFT, sigma=1e-7, mic_d=0.01, mask="ipd", postfilter="none",
+        plan = avz.MVDRPlan(n_fft=n_fft, sigma=1e-7, mic_d=0.01, mask="ipd", postfilter="none",
                             normalize=norm, norm_eps=1e-6, max_batch=B, max_samples=S)
         streams = 2
-    refs = {}
-    if args.workload == "ibm":
-        refs = dict(ref_tgt=d_tgt, ref_int=d_itf)
     lens = torch.full((B,), S, dtype=torch.int32, device=dev)
-    out = plan.alloc_out(B, S, dev)
-    peak = torch.empty((B,), dtype=torch.float32, device=dev)
+    sets = []
+    for d_mix, d_tgt, d_itf in batches:
+        refs = dict(ref_tgt=d_tgt, ref_int=d_itf) if spec["workload"] == "ibm" else {}
+        sets.append(dict(mix=d_mix, refs=refs, out=plan.alloc_out(B, S, dev),
+                         peak=torch.empty((B,), dtype=torch.float32, device=dev)))
+    it = [0]
 
     def step():
-        plan.run(d_mix, lens, max_len=S, out=out, peak=peak, **refs)
+        s = sets[it[0] % len(sets)]
+        it[0] += 1
+        plan.run(s["mix"], lens, max_len=S, out=s["out"], peak=s["peak"], **s["refs"])
 
     n_out = plan.out_len(S)
-    F, T = N_FFT // 2 + 1, -(-S // HOP) + 1
-    info = dict(plan=plan, out=out[:, :min(n_out, S)], peak=peak, bins=B * F * T,
+    F, T = n_fft // 2 + 1, -(-S // hop) + 1
+    s0 = sets[0]
+    info = dict(plan=plan, out=s0["out"][:, :min(n_out, S)], peak=s0["peak"], bins=B * F * T,
                 alg_analysis=B * streams * S * 4, alg_chain=B * (streams * S * 4 + n_out * 4),
-                kernel=f"avz_analysis_kernel<{N_FFT},{'IBM' if args.workload == 'ibm' else 'IPD'}>",
-                mix=d_mix, refs=refs)
+                kernel=f"avz_analysis_kernel<{n_fft},{'IBM' if spec['workload'] == 'ibm' else 'IPD'}>",
+                mix=s0["mix"], refs=s0["refs"], sets=sets, it=it)
     return step, info
 
 
-def setup_unet(args, B, S, dev, d_mix):
+def setup_unet(spec, dev, batches, unet_dtype):
     import torch
 
     from avz import neural as N
     torch.manual_seed(20250101)
     model = N.FreqPreservingUNet().eval().to(dev)
+    B, S = spec["B"], int(SECONDS * FS)
     n_items = B * -(-S // 16000)
-    dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[args.unet_dtype]
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[unet_dtype]
     bf = N.NeuralMaskBeamformer(model, max_items=n_items, model_dtype=dt)
     y = {}
+    it = [0]
 
     def step():
+        d_mix = batches[it[0] % len(batches)][0]
+        it[0] += 1
         y["out"], _ = bf.run(d_mix)
 
-    F = N_FFT // 2 + 1
-    Tc = -(-bf.chunk // HOP) + 1
+    n_fft = spec["n_fft"]
+    F = n_fft // 2 + 1
+    Tc = -(-bf.chunk // (n_fft // 2)) + 1
     n_out = bf.plan.out_len(bf.chunk)
     info = dict(plan=bf.plan, bf=bf, bins=n_items * F * Tc, n_items=n_items,
                 alg_analysis=n_items * 2 * bf.chunk * 4,
                 alg_chain=n_items * (2 * bf.chunk * 4 + n_out * 4),
-                kernel=f"avz_analysis_kernel<{N_FFT},EXTERNAL>", mix=d_mix, y=y)
+                kernel=f"avz_analysis_kernel<{n_fft},EXTERNAL>", mix=batches[0][0], y=y, it=it)
     return step, info
 
 
-def main():
-    global N_FFT, HOP
-    args = parse()
-    N_FFT, HOP = args.n_fft, args.n_fft // 2
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    S = int(SECONDS * FS)
-    B = args.batch
+def setup_chain4(spec, dev, batches):
+    """configs[4]'s MVDR chain alone: the batch's 2-s chunk items (avz_chunk_split) through
+    the external-mask chain with a fixed synthetic target mask (what the U-Net would hand
+    over), one avz_mvdr_batch call per step."""
+    import torch
 
-    from avz import synth
-    gen_host = synth.make_batch_philox if args.scenes == "philox" else synth.make_batch
+    from avz import neural as N
+    bf = N.NeuralMaskBeamformer(torch.nn.Identity(), max_items=spec["B"] * 4)
+    sets = []
+    for d_mix, _, _ in batches:
+        items = bf.split(d_mix)[0]
+        F, T = bf.plan.cfg.n_fft // 2 + 1, bf.plan.frames(bf.chunk)
+        g = torch.Generator(device=dev).manual_seed(7)
+        mask = torch.rand((items.shape[0], F, T), generator=g, device=dev)
+        n = items.shape[0]
+        sets.append(dict(items=items, mask=mask, out=bf.plan.alloc_out(n, bf.chunk, dev),
+                         peak=torch.empty((n,), dtype=torch.float32, device=dev),
+                         lens=torch.full((n,), bf.chunk, dtype=torch.int32, device=dev)))
+    it = [0]
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and args.workload != "unet":
-        workers = args.cpu_workers or min(16, len(os.sched_getaffinity(0)))
-        k = min(B, 32)
-        # the host restatement of the same scenes (forked before any GPU initialisation)
-        sample = gen_host(k, start=rank * B, n_samples=S, n_interferers=args.interferers)
-        cpu = cpu_baseline(sample, args.cpu_seconds, workers, args.workload)
+    def step():
+        s = sets[it[0] % len(sets)]
+        it[0] += 1
+        bf.plan.run(s["items"], s["lens"], max_len=bf.chunk, ext_mask=s["mask"], out=s["out"],
+                    peak=s["peak"])
 
+    n = sets[0]["items"].shape[0]
+    F, T = bf.plan.cfg.n_fft // 2 + 1, bf.plan.frames(bf.chunk)
+    n_out = bf.plan.out_len(bf.chunk)
+    info = dict(plan=bf.plan, bins=n * F * T, n_items=n, alg_analysis=n * 2 * bf.chunk * 4,
+                alg_chain=n * (2 * bf.chunk * 4 + n_out * 4 + F * T * 4),
+                kernel=f"avz_analysis_kernel<{bf.plan.cfg.n_fft},EXTERNAL>", it=it)
+    return step, info
+
+
+def run_timed(step, plan, K, W, world, dev, settle_on, kernel_timing):
+    """Clock settling, W warmup steps, K timed steps (barrier + synchronize on both sides),
+    then an untimed pass with HIP events around all four kernels."""
     import torch
     import torch.distributed as dist
-
-    from avz import metrics
-    from oracle import avz_oracle as O
-
-    # --rehearse-shared-gpu: every rank on cuda:0 with gloo, to exercise the N > 1 code
-    # path (sharding, metric all-reduce, max-over-ranks timing) on a one-GPU box
-    gpu = 0 if args.rehearse_shared_gpu else local
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    if world > 1:
-        if args.rehearse_shared_gpu:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
-
-    # this rank's shard of utterances rank * B .. rank * B + B - 1, generated in HBM
-    g0 = time.perf_counter()
-    if args.scenes == "philox":
-        d_mix, d_tgt, d_itf = synth.make_batch_device(B, start=rank * B, n_samples=S,
-                                                      n_interferers=args.interferers,
-                                                      device=dev, rng="philox")
-    else:
-        hm, ht, hi = synth.make_batch(B, start=rank * B, n_samples=S,
-                                      n_interferers=args.interferers)
-        d_mix, d_tgt, d_itf = (torch.from_numpy(a).to(dev) for a in (hm, ht, hi))
-    torch.cuda.synchronize()
-    gen_ms = 1e3 * (time.perf_counter() - g0)
-
-    if args.workload == "unet":
-        step, info = setup_unet(args, B, S, dev, d_mix)
-    else:
-        step, info = setup_chain(args, B, S, dev, d_mix, d_tgt, d_itf)
-    plan = info["plan"]
-
     # Clock settling: a GPU that sat idle (host scene setup, the CPU baseline) runs its
     # compute-bound kernels 10-15 % slower for the first tens of milliseconds of load
     # (profiles/r02u/warmup_sensitivity.txt). Untimed blocks of SETTLE_BLOCK steps run for at
     # least SETTLE_MIN_S and until two consecutive blocks agree within 1 % (at most
-    # SETTLE_MAX_S; a 20-step block alone converged early at 85.6 vs 89.7 G), so the K timed steps
-    # measure the steady state a continuous job runs at; the first block's per-step time
-    # is reported as settle.cold_ms_per_step beside the steady-state value.
+    # SETTLE_MAX_S), so the K timed steps measure the steady state a continuous job runs at;
+    # the first block's per-step time is reported as settle.cold_ms_per_step.
     settle = {"steps": 0, "ms": 0.0, "cold_ms_per_step": None}
-    if not args.no_settle and args.workload != "unet":  # a U-Net step alone takes ~1.4 s
+    if settle_on:
         s0 = time.perf_counter()
         step()  # first launch (code objects, attributes) outside the cold measurement
         settle["steps"] = 1
@@ -299,12 +336,11 @@ def main():
             if done or time.perf_counter() - s0 > SETTLE_MAX_S:
                 break
         settle["ms"] = 1e3 * (time.perf_counter() - s0)
-    for _ in range(args.warmup):
+    for _ in range(W):
         step()
     torch.cuda.synchronize()
 
-    K = args.steps
-    if not args.no_kernel_timing:
+    if kernel_timing:
         plan.set_timing(True, analysis_only=True, period=TIMING_PERIOD)
     # No torch events inside the timed loop: a default torch.cuda.Event record is a
     # system-scope release (an L2 writeback, ~15 us between steps on MI355X). The plan's
@@ -316,26 +352,104 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(K):
+    for _ in range(K):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    step_ms = 1e3 * (t1 - t0) / K
     kt = None
-    if not args.no_kernel_timing:
+    if kernel_timing:
         dom = plan.timing()  # the bracketed steps among the K timed ones
-        dom_timed, dom_calls = dom["analysis"], dom["calls"]
-        # every kernel of the chain: a separate, untimed pass with events around all four
-        plan.set_timing(True)
+        plan.set_timing(True)  # every kernel of the chain: a separate, untimed pass
         for _ in range(max(3, K // 4)):
             step()
         kt = plan.timing()
         plan.set_timing(False)
-        kt["analysis_timed"] = dom_timed
-        kt["analysis_timed_calls"] = dom_calls
+        kt["analysis_timed"] = dom["analysis"]
+        kt["analysis_timed_calls"] = dom["calls"]
+    return t1 - t0, kt, settle
+
+
+def secondary_entry(spec, info, K, elapsed, kt, world):
+    """A secondary configuration's figures, measured as the headline's."""
+    value = world * info["bins"] * K / elapsed
+    bpb = bytes_per_bin(spec["workload"], spec["n_fft"])
+    e = {"config": spec["text"], "value": value, "unit": "TF-bins/s",
+         "ms_per_step": 1e3 * elapsed / K,
+         "frac": value / world * bpb / 1e9 / HBM_PEAK_GBS, "bytes_per_bin": bpb,
+         "tf_bins_per_step": info["bins"]}
+    if kt:
+        e["kernels_ms"] = {k: kt[k] for k in info["plan"].KERNELS}
+        dom_ms = kt["analysis_timed"]
+        e["dominant_kernel"] = {"kernel": info["kernel"], "kernel_ms": dom_ms,
+                                "frac": info["alg_analysis"] / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    return e
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    S = int(SECONDS * FS)
+    B = args.batch
+    N_FFT, HOP = args.n_fft, args.n_fft // 2
+
+    from avz import synth
+    gen_host = synth.make_batch_philox if args.scenes == "philox" else synth.make_batch
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and args.workload != "unet":
+        available = len(os.sched_getaffinity(0))
+        workers = args.cpu_workers or min(CPU_SHARE, available)
+        k = min(B, 32)
+        # the host restatement of the same scenes (forked before any GPU initialisation)
+        sample = gen_host(k, start=rank * B, n_samples=S, n_interferers=args.interferers)
+        cpu = cpu_baseline(sample, args.cpu_seconds, workers, args.workload, N_FFT, available)
+
+    import torch
+    import torch.distributed as dist
+
+    from avz import metrics
+    from oracle import avz_oracle as O
+
+    # --rehearse-shared-gpu: every rank on cuda:0 with gloo, to exercise the N > 1 code
+    # path (sharding, metric all-reduce, max-over-ranks timing) on a one-GPU box
+    gpu = 0 if args.rehearse_shared_gpu else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    if world > 1:
+        if args.rehearse_shared_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+
+    spec = dict(workload=args.workload, B=B, k=args.interferers, n_fft=N_FFT,
+                normalize=args.normalize)
+    # this rank's shard(s) of utterances, generated in HBM: batch 0 = utterances rank * B ..
+    # rank * B + B - 1 (the one the SIR metrics score), batch 1 = the next world * B
+    g0 = time.perf_counter()
+    n_sets = 1 if args.single_batch else 2
+    batches = [gen_batch(spec, dev, i * world * B + rank * B, args.scenes) for i in range(n_sets)]
+    torch.cuda.synchronize()
+    gen_ms = 1e3 * (time.perf_counter() - g0)
+    d_mix, d_tgt, d_itf = batches[0]
+
+    if args.workload == "unet":
+        step, info = setup_unet(spec, dev, batches, args.unet_dtype)
+    else:
+        step, info = setup_chain(spec, dev, batches)
+    plan = info["plan"]
+    K = args.steps
+    # a U-Net step alone takes ~1.4 s: no settling blocks for it
+    elapsed_s, kt, settle = run_timed(step, plan, K, args.warmup, world, dev,
+                                      not args.no_settle and args.workload != "unet",
+                                      not args.no_kernel_timing)
+    elapsed = torch.tensor([elapsed_s], dtype=torch.float64, device=dev)
+    step_ms = 1e3 * elapsed_s / K
     chain_ms = sum(kt[k] for k in plan.KERNELS) if kt else step_ms
 
     extra = {}
@@ -368,6 +482,7 @@ def main():
             torch.cuda.synchronize()
             p0 = time.perf_counter()
             for _ in range(n_pcie):
+                info["it"][0] = 0  # batch 0: the buffers being refilled
                 for h, d in d_in:
                     d.copy_(h, non_blocking=True)
                 step()
@@ -383,6 +498,10 @@ def main():
             extra["pcie_inclusive"] = {"error": repr(exc)[:200]}
 
     # ---- final metrics: projection SIR per utterance (run_metrics.py:6-36), RCCL all-reduce
+    # of batch 0's outputs: one more step on batch 0 leaves them in its output buffer
+    info["it"][0] = 0
+    step()
+    torch.cuda.synchronize()
     L = S
     if args.workload == "unet":
         est_out = info["y"]["out"][:, :L]
@@ -427,12 +546,8 @@ def main():
 
     t_max = float(elapsed.item())
     value = world * info["bins"] * K / t_max
-    # Roofline, SURVEY 8(d): achieved = TF-bins/s x bytes_per_bin with bytes_per_bin =
-    # (fp32 streams) x 4 H / F: every 4-byte sample stream costs 4 H / F B per TF-bin
-    # (3.992 at 1024/512). ibm: 2 mic + 2 references + output = 19.96 B/bin; ipd: 2 mic +
-    # output = 11.98; external mask: + 4 B/bin of mask = 15.98. Per GPU (peak is per GPU).
-    per_stream = 4.0 * HOP / (N_FFT // 2 + 1)
-    bpb = {"ibm": 5 * per_stream, "ipd": 3 * per_stream, "unet": 3 * per_stream + 4.0}[args.workload]
+    # Roofline, SURVEY 8(d): achieved = TF-bins/s x bytes_per_bin, per GPU (peak is per GPU).
+    bpb = bytes_per_bin(args.workload, N_FFT)
     alg_analysis, alg_chain = info["alg_analysis"], info["alg_chain"]
     traffic = {}
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -467,6 +582,45 @@ def main():
         roof["chain_events"] = {"ms": chain_ms, "alg_bytes_per_launch": alg_chain,
                                 "achieved": alg_chain / (chain_ms * 1e-3) / 1e9,
                                 "frac": alg_chain / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+    # ---- the other single-GPU configurations, same method, same line (N = 1 default run)
+    secondary = None
+    default_run = (args.workload == "ibm" and N_FFT == 1024 and B == 256 and args.interferers == 2
+                   and args.normalize == "peak")
+    if world == 1 and default_run and not args.no_secondary:
+        del batches, d_mix, d_tgt, d_itf, est, m, info, step
+        torch.cuda.empty_cache()
+        secondary = {}
+        specs = [
+            ("configs[2]_shard", dict(workload="ibm", B=512, k=3, n_fft=1024, normalize="peak",
+                                       text="configs[2] per-GPU shard: B=4096 over 8 GPUs = 512 "
+                                            "utterances, 3 interferers, oracle IBM, 1024/512")),
+            ("configs[3]", dict(workload="ipd", B=1024, k=2, n_fft=1024, normalize="peak",
+                                text="configs[3]: B=1024, heuristic IPD mask, sigma 1e-7, no "
+                                     "post-filter, 1024/512")),
+            ("n_fft_512", dict(workload="ibm", B=256, k=2, n_fft=512, normalize="peak",
+                               text="configs[1] at oracle_debug's 512/256 STFT (Fft512x2)")),
+            ("deferred_norm", dict(workload="ibm", B=256, k=2, n_fft=1024, normalize="deferred",
+                                   text="configs[1], the batch driver's deferred normalisation "
+                                        "(un-normalised output + peak[B])")),
+            ("configs[4]_chain", dict(workload="chain4", B=1024, k=2, n_fft=1024, normalize="none",
+                                      text=WORKLOAD_TEXT["chain4"].format(B=1024, n=1024, h=512))),
+        ]
+        for name, sp in specs:
+            try:
+                bs = [gen_batch(sp, dev, i * sp["B"], args.scenes) for i in range(n_sets)]
+                if sp["workload"] == "chain4":
+                    st, inf = setup_chain4(sp, dev, bs)
+                else:
+                    st, inf = setup_chain(sp, dev, bs)
+                el, ktx, _ = run_timed(st, inf["plan"], K, args.warmup, 1, dev,
+                                       not args.no_settle, not args.no_kernel_timing)
+                secondary[name] = secondary_entry(sp, inf, K, el, ktx, 1)
+                del bs, st, inf
+                torch.cuda.empty_cache()
+            except Exception as exc:  # a side figure must never sink the bench line
+                secondary[name] = {"error": repr(exc)[:300]}
+
     if rank == 0:
         wtext = WORKLOAD_TEXT[args.workload].format(
             B=B, k=args.interferers, unet_dtype=args.unet_dtype, n=N_FFT, h=HOP)
@@ -476,12 +630,13 @@ def main():
         cfg = {"workload": wtext,
                "batch_per_gpu": B, "global_batch": B * world, "samples": S,
                "n_fft": N_FFT, "hop": HOP, "parallelism":
-               f"utterance-sharded x{world}, RCCL metric all-reduce only"}
+               f"utterance-sharded x{world}, RCCL metric all-reduce only",
+               "input_batches": n_sets}
         if args.workload == "ibm":
-            cfg.update(tf_bins_per_utt=info["bins"] // B, sigma=1.0, mask="ibm",
+            cfg.update(tf_bins_per_utt=info_bins_per(B, N_FFT, S), sigma=1.0, mask="ibm",
                        postfilter="ibm", normalize=args.normalize)
         elif args.workload == "ipd":
-            cfg.update(tf_bins_per_utt=info["bins"] // B, sigma=1e-7, mask="ipd",
+            cfg.update(tf_bins_per_utt=info_bins_per(B, N_FFT, S), sigma=1e-7, mask="ipd",
                        postfilter="none", normalize=args.normalize)
         else:
             cfg.update(chunk_items=info["n_items"], tf_bins_per_chunk=info["bins"] // info["n_items"],
@@ -494,7 +649,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": ("synthetic speech-like 2-mic far-field mixtures (SURVEY 8(d) model), "
                      + ("generated in HBM by avz_scene_generate (Philox draws keyed by utterance "
-                        f"index rank*B+b; {gen_ms:.1f} ms for this rank's shard)"
+                        f"index; {n_sets} batches of B per rank alternating over the timed steps; "
+                        f"{gen_ms:.1f} ms for this rank's)"
                         if args.scenes == "philox" else
                         f"host numpy generator, seeds 1000+idx ({gen_ms:.0f} ms incl. H2D)")),
             "config": cfg,
@@ -505,9 +661,16 @@ def main():
                     "sir_abs_delta_vs_reference_db": d_sir, "n_utts": int(sums[2])},
         }
         line.update(extra)
+        if secondary is not None:
+            line["secondary"] = secondary
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def info_bins_per(B, n_fft, S):
+    hop = n_fft // 2
+    return (n_fft // 2 + 1) * (-(-S // hop) + 1)
 
 
 if __name__ == "__main__":
