@@ -414,6 +414,7 @@ def main():
     import torch.distributed as dist
 
     from avz import metrics
+    from avz.batch_run import allreduce_job
     from oracle import avz_oracle as O
 
     # --rehearse-shared-gpu: every rank on cuda:0 with gloo, to exercise the N > 1 code
@@ -519,16 +520,15 @@ def main():
     sir_out, sir_in = m[:B, 3], m[B:, 3]
     sums = torch.stack([sir_in.sum(), sir_out.sum(), torch.tensor(float(B), device=dev,
                                                                   dtype=torch.float64)])
-    if world > 1:
-        dist.all_reduce(sums)
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    if world > 1:  # SUM of the metric sums, MAX over ranks of the timings
         kn = plan.KERNELS + ("analysis_timed",)
-        mx = torch.tensor([step_ms, chain_ms] + ([kt[k] for k in kn] if kt else []),
+        mx = torch.tensor([elapsed_s, step_ms, chain_ms] + ([kt[k] for k in kn] if kt else []),
                           dtype=torch.float64, device=dev)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        step_ms, chain_ms = float(mx[0]), float(mx[1])
+        allreduce_job(sums, mx)
+        elapsed = mx[:1]
+        step_ms, chain_ms = float(mx[1]), float(mx[2])
         if kt:
-            kt.update({k: float(mx[2 + j]) for j, k in enumerate(kn)})
+            kt.update({k: float(mx[3 + j]) for j, k in enumerate(kn)})
     # SIR delta vs the reference restatement on identical inputs (rank 0, few utterances)
     d_sir = None
     if rank == 0 and args.workload != "unet":

@@ -37,7 +37,7 @@ extern "C" {
 #define AVZ_ERR_SHAPE (-2)       /* length/stride/batch outside the plan        */
 #define AVZ_ERR_HIP (-3)         /* HIP runtime error (launch / allocation)     */
 #define AVZ_ERR_UNSUPPORTED (-4) /* configuration not implemented              */
-#define AVZ_ERR_ALIGN (-5)       /* output/stride not 16-byte aligned           */
+#define AVZ_ERR_ALIGN (-5)       /* pointer/stride below its element/vector alignment */
 
 /* mask sources */
 #define AVZ_MASK_IBM 0      /* oracle ideal binary mask from refs, oracle_debug.py:49-53  */
@@ -177,7 +177,8 @@ int avz_apply_istft(const avz_plan* plan, const avz_batch_args* args, const floa
  * mode must be AVZ_MASK_EXTERNAL (mask = target probability, noise weight 1 - M).
  * Y: complex64 [b][m][k][t] (interleaved re/im; m = mic 0, 1; t contiguous), strides in
  * complex elements; mask [b][k][t] float; S: complex64 [b][k][t]. steer: optional [F][2]
- * complex128 (batch_mvdr's d_vectors; NULL: the plan's table). cov_out / w_out: optional
+ * complex128 (batch_mvdr's d_vectors; NULL: the plan's table). Y and S 8-byte, mask 4-byte
+ * aligned (else AVZ_ERR_ALIGN). cov_out / w_out: optional
  * per-bin covariance sums / weights; fallback: optional [batch] int flags (1 where an
  * item took the item-level fallback; NULL: the plan's own buffer). */
 typedef struct avz_spectral_args {

@@ -418,6 +418,40 @@ def neural_deploy_vec(y: np.ndarray, masks, chunk: int = 32000, n_fft: int = 102
     return out_buf[:S] / norm_buf[:S]
 
 
+def process_audio_file_vec(y: np.ndarray, masks, chunk: int = 32000, n_fft: int = 1024,
+                           d: float = 0.04, c: float = C_SOUND, sigma: float = 1e-5,
+                           fs: int = FS) -> np.ndarray:
+    """rt_av_zoom/core/tf_lite_version/inference.py:245-391 (process_audio_file minus file
+    I/O, timing prints and the TFLite model): y [S, 2]; masks[i] the target mask of chunk i
+    (TFLiteBeamformer.predict_mask's output, :300). Chunks of ``chunk`` samples every
+    chunk // 2, ceil(S / hop) of them, zero-padded tail (:269-289); stft (:293); batch_mvdr
+    with the module's steering vectors (:320-327); S * max(M, 0.05) and the whole istft output
+    (:341-345, 32256 samples for a 32000-sample chunk) overlap-added at the chunk start,
+    clipped at the end of the buffer, with a per-sample count (:349-355); out / count
+    (count 0 -> 1) and peak normalisation + 1e-9 (:361-365)."""
+    hop_c = chunk // 2
+    S = y.shape[0]
+    out_buf = np.zeros(S)
+    norm_buf = np.zeros(S)
+    for i in range(int(np.ceil(S / hop_c))):
+        start = i * hop_c
+        seg = y[start:start + chunk]
+        if len(seg) < chunk:
+            seg = np.pad(seg, ((0, chunk - len(seg)), (0, 0)))
+        f_bins, _, Y = stft(seg.T, fs=fs, nperseg=n_fft, noverlap=n_fft // 2)
+        M = np.asarray(masks[i])
+        mf, mt = min(M.shape[0], Y.shape[1]), min(M.shape[1], Y.shape[2])
+        M, Y, fv = M[:mf, :mt], Y[:, :mf, :mt], f_bins[:mf]
+        S_out = batch_mvdr(Y, M, fv, get_all_steering_vectors(fv, ANGLE_TARGET, d, c), sigma)
+        _, xo = istft(S_out * np.maximum(M, 0.05), fs=fs, nperseg=n_fft, noverlap=n_fft // 2)
+        w = min(len(xo), S - start)
+        out_buf[start:start + w] += xo[:w]
+        norm_buf[start:start + w] += 1.0
+    norm_buf[norm_buf == 0] = 1.0
+    final = out_buf / norm_buf
+    return final / (np.max(np.abs(final)) + 1e-9)
+
+
 # ----------------------------------------------------------------------------
 # Final_pipeline: hybrid hard-null beamformer + 2-s chunked overlap-add driver
 # ----------------------------------------------------------------------------

@@ -88,6 +88,9 @@ class AvzError(RuntimeError):
     pass
 
 
+ABI_VERSION = 2
+
+
 def hip_runtimes_mapped() -> list:
     """Paths of every libamdhip64 mapped into this process."""
     paths = set()
@@ -156,6 +159,9 @@ def _load():
                  "avz_srp_scan", "avz_projection_metrics", "avz_scene_mix",
                  "avz_scene_generate", "avz_projection_metrics_scaled", "avz_version"):
         getattr(lib, name).restype = ct.c_int
+    if lib.avz_version() != ABI_VERSION:  # the struct layouts above are version 2's
+        raise ImportError(f"libavz ABI version {lib.avz_version()} != {ABI_VERSION} "
+                          "(AvzBatchArgs / AvzSpectralArgs layouts); rebuild")
     return lib
 
 

@@ -38,6 +38,18 @@ def shard(n: int, rank: int, world: int):
     return start, start + base + (1 if rank < rem else 0)
 
 
+def allreduce_job(sums: torch.Tensor, maxes: torch.Tensor | None = None):
+    """The job's only collectives: SUM of the metric sums and MAX of the
+    per-rank timings (bench.py's max-over-ranks step time), in place. Every rank of a
+    process group calls it -- RCCL over xGMI on GPUs, gloo in CPU tests; a one-rank group
+    runs them too (identity results). No-op without a process group."""
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(sums)
+        if maxes is not None:
+            dist.all_reduce(maxes, op=dist.ReduceOp.MAX)
+    return sums, maxes
+
+
 def world_info():
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
@@ -120,8 +132,7 @@ def run_batch(n_runs: int, start_idx: int = 0, n_interferers: int = 2, *,
                          "SIR_Enh": f"{vals[1, j]:.2f}", "SIR_Imp": f"{vals[1, j] - vals[0, j]:.2f}",
                          "SINR_Base": f"{vals[2, j]:.2f}", "SINR_Enh": f"{vals[3, j]:.2f}",
                          "STOI": "0.0000", "PESQ_WB": "0.0000", "PESQ_NB": "0.0000"})
-    if world > 1:
-        dist.all_reduce(sums)  # the only collective: metric sums
+    allreduce_job(sums)  # the only collective: metric sums
     if csv_path is not None:
         append_csv(csv_path, rows, rank, world)
     return BatchResult(rows=rows, sums=sums.cpu().numpy())

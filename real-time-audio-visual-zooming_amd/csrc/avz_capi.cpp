@@ -113,9 +113,13 @@ extern "C" const char* avz_strerror(int code) {
     case AVZ_ERR_SHAPE: return "length, stride or batch outside the plan";
     case AVZ_ERR_HIP: return "HIP runtime error";
     case AVZ_ERR_UNSUPPORTED: return "unsupported configuration";
-    case AVZ_ERR_ALIGN: return "output pointer/stride not 16-byte aligned";
+    case AVZ_ERR_ALIGN: return "pointer or stride not aligned to its element / vector size";
     default: return "unknown error";
   }
+}
+
+static bool misaligned(const void* ptr, uintptr_t bytes) {
+  return (reinterpret_cast<uintptr_t>(ptr) & (bytes - 1)) != 0;
 }
 
 static int frames_for(int len, int hop) { return (len + hop - 1) / hop + 1; }
@@ -316,6 +320,11 @@ static int prepare_chain(const avz_plan* p, const avz_batch_args* a, int use, av
   k.peak_u = ws.peak_u;
   k.flag = ws.flag;
   k.pf_gain = ws.pf_gain;
+  if (use == USE_COVARIANCE) {  // that stage produces cov_out only: leave the caller's
+    k.out = nullptr;            // out / peak / w buffers untouched (the analysis kernel
+    k.peak = nullptr;           // would otherwise zero peak[b] as the atomicMax target)
+    k.w_out = nullptr;
+  }
   return AVZ_OK;
 }
 
@@ -372,6 +381,7 @@ extern "C" int avz_istft(const avz_plan* p, int batch, int frames, const float* 
   if (batch < 0 || batch > c.max_batch || frames < 0) return AVZ_ERR_SHAPE;
   if (batch == 0) return AVZ_OK;
   if (!S || !out) return AVZ_ERR_ARG;
+  if (misaligned(S, 8)) return AVZ_ERR_ALIGN;
   const long long len = (long long)(frames - 1) * c.hop;  // scipy.signal.istft output length
   if (len < c.n_fft || len > c.max_samples) return AVZ_ERR_SHAPE;
   const int F = c.n_fft / 2 + 1;
@@ -415,6 +425,9 @@ extern "C" int avz_beamform_spectral(const avz_plan* p, const avz_spectral_args*
   if (a->batch < 0 || a->batch > c.max_batch || a->frames < 1) return AVZ_ERR_SHAPE;
   if (a->batch == 0) return AVZ_OK;
   if (!a->Y || !a->mask || !a->S) return AVZ_ERR_ARG;
+  // complex64 Y / S (8 B), float mask (4 B): element-aligned, or a GPU fault
+  if (misaligned(a->Y, 8) || misaligned(a->S, 8) || misaligned(a->mask, 4))
+    return AVZ_ERR_ALIGN;
   if (c.mask_mode != AVZ_MASK_EXTERNAL) return AVZ_ERR_ARG;  // the mask is a target probability
   const int F = c.n_fft / 2 + 1;
   if (a->y_stride_f < a->frames || a->y_stride_m < (long long)F * a->y_stride_f ||
@@ -452,7 +465,7 @@ extern "C" int avz_solve_covariance(const avz_plan* p, int batch, const double* 
   if (batch < 0 || batch > p->cfg.max_batch) return AVZ_ERR_SHAPE;
   if (batch == 0) return AVZ_OK;
   if (!cov || !w) return AVZ_ERR_ARG;
-  if (reinterpret_cast<uintptr_t>(w) & 15) return AVZ_ERR_ALIGN;
+  if (misaligned(cov, 8) || misaligned(w, 16) || misaligned(steer, 8)) return AVZ_ERR_ALIGN;
   avz::ChainArgs k{};
   plan_params(p, k);
   avz::SpecArgs s{};
@@ -726,6 +739,8 @@ extern "C" long long avz_scene_generate_workspace_bytes(int batch, int n_interfe
   return avz_scene_gen_ws(batch, 1 + n_interferers, n);
 }
 
+constexpr int kMaxInterferers = 254;
+
 extern "C" int avz_scene_generate(int batch, long long start_idx, int n_interferers, int n,
                                   unsigned seed, double mic_d, double c_sound, double fs,
                                   double sir_db, double snr_db, float* mix, long long mix_stride,
@@ -733,6 +748,9 @@ extern "C" int avz_scene_generate(int batch, long long start_idx, int n_interfer
                                   long long ref_stride, void* workspace,
                                   long long workspace_bytes, void* stream) {
   if (n_interferers < 0 || start_idx < 0) return AVZ_ERR_ARG;
+  // source s draws Philox stream s and mic noise streams 0x100 + mic: at most 255
+  // interferers keep them disjoint; fs >= 4 keeps the 0.25-s envelope block non-empty
+  if (n_interferers > kMaxInterferers || !(fs >= 4.0)) return AVZ_ERR_ARG;
   const int n_src = 1 + n_interferers;
   const int rc0 = scene_check(batch, n_src, n, fs, c_sound, mix, mix_stride, ch_stride, tgt, itf,
                               ref_stride, workspace);

@@ -285,8 +285,13 @@ __device__ __forceinline__ void mvdr_weights_d(const double (&c)[5], int k, int 
     const double det = a * e - (br * br + bi * bi);
     double t0r, t0i, t1r, t1i;
     bool solved = true;
-    if (det == 0.0 || !isfinite(det)) {
-      if (singular) *singular = (det == 0.0);
+    if (!isfinite(det)) {
+      // NaN / Inf in Y or the mask: LAPACK's gesv (np.linalg.solve / inv) raises only on an
+      // exactly zero pivot, so the reference returns NaN weights here in every mode
+      w0r = w0i = w1r = w1i = __builtin_nan("");
+      solved = false;
+    } else if (det == 0.0) {
+      if (singular) *singular = true;
       if (A.singular_fallback == 1) {  // oracle_reverb.py:133-135: ones(n)/n, not normalised
         w0r = 0.5;
         w1r = 0.5;

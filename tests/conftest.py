@@ -37,3 +37,33 @@ def gpu_device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+def hybrid_bin_causes(Y, M, f, bins, matches, cnt=None):
+    """Explain every hybrid hard-null bin in ``bins`` whose engine result differs from the
+    reference/oracle (Final_pipeline/src/inference.py:28-98): (a) a different noise-frame
+    count (``cnt``: the engine's per-bin counts; IBM ties of the fp32 STFT), (b) a
+    near-degenerate principal eigenvector (relative eigen-gap < 1e-4: the direction is
+    ill-conditioned), or (c) the cond_2 <= cond_max branch decided the other way within
+    rounding: ``matches(k, w)`` must accept the oracle weights of the forced other branch.
+    Anything else fails. Returns the cause counts."""
+    from oracle import avz_oracle as O
+    Yd = Y.astype(np.complex128)
+    m = (1.0 - M).astype(np.float64)
+    nrm = m.sum(axis=1) + 1e-6
+    a = np.einsum("ft,ft->f", m, np.abs(Yd[0]) ** 2) / nrm
+    e = np.einsum("ft,ft->f", m, np.abs(Yd[1]) ** 2) / nrm
+    b = np.einsum("ft,ft->f", m, Yd[0] * Yd[1].conj()) / nrm
+    gap = 2 * np.sqrt((0.5 * (a - e)) ** 2 + np.abs(b) ** 2) / np.maximum(a + e, 1e-300)
+    causes = {"mask count": 0, "eigen-gap": 0, "cond branch": 0}
+    for k in bins:
+        if cnt is not None and cnt[k] != m[k].sum():
+            causes["mask count"] += 1
+        elif gap[k] < 1e-4:
+            causes["eigen-gap"] += 1
+        else:
+            alt = [O.hybrid_weights_vec(Y[:, k:k + 1], M[k:k + 1], f[k:k + 1], cond_max=cm)[0]
+                   for cm in (1e300, -1.0)]
+            assert any(matches(k, w) for w in alt), (k, gap[k])
+            causes["cond branch"] += 1
+    return causes

@@ -20,7 +20,7 @@ module is injected (only TFLiteBeamformer uses it, and that class is replaced by
 _MaskFeeder below because the .tflite model file is absent).
 
 Usage:  python tests/golden/make_golden.py [hybrid] [srp] [report] [reverb] [neural] [world]
-        [spectral]
+        [spectral] [tflite]
         (writes tests/golden/*.npz)
 """
 from __future__ import annotations
@@ -540,6 +540,83 @@ def gen_spectral(trip, save):
              chunk_out=chunk_out.astype(np.float32), fallback=bool(raised))
 
 
+class _TLMaskFeeder:
+    """Stand-in for tf_lite_version's TFLiteBeamformer (inference.py:185-239): the
+    .tflite model is absent and TensorFlow is not installed, so predict_mask(log_mag, ipd)
+    returns the next chunk's precomputed target mask and records the features the
+    reference computed for it (:296-300)."""
+    masks: list = []
+    features: list = []
+
+    def __init__(self, model_path="mask_estimator.tflite"):
+        self.i = 0
+
+    def predict_mask(self, log_mag, ipd):
+        _TLMaskFeeder.features.append((np.array(log_mag), np.array(ipd)))
+        m = _TLMaskFeeder.masks[self.i]
+        self.i += 1
+        return m
+
+
+def chunk_soft_masks(tgt, itf, n_total, chunk=32000, hop=16000, n_fft=1024):
+    """Per-chunk soft target masks sigmoid(log|S_t| - log|S_i|) (float32, like a TFLite
+    output) with process_audio_file's chunking (inference.py:269-289)."""
+    masks = []
+    for c in range(int(np.ceil(n_total / hop))):
+        seg_t = np.pad(tgt[c * hop:c * hop + chunk], (0, max(0, chunk - len(tgt[c * hop:c * hop + chunk]))))
+        seg_i = np.pad(itf[c * hop:c * hop + chunk], (0, max(0, chunk - len(itf[c * hop:c * hop + chunk]))))
+        _, _, St = scipy.signal.stft(seg_t, fs=16000, nperseg=n_fft, noverlap=n_fft - n_fft // 2)
+        _, _, Si = scipy.signal.stft(seg_i, fs=16000, nperseg=n_fft, noverlap=n_fft - n_fft // 2)
+        z = np.log(np.abs(St) + 1e-7) - np.log(np.abs(Si) + 1e-7)
+        masks.append((1.0 / (1.0 + np.exp(-z))).astype(np.float32))
+    return masks
+
+
+def gen_tflite(trip, run_metrics, save):
+    """rt_av_zoom/core/tf_lite_version/inference.py process_audio_file (:245-391) run on
+    each bundled stereo mixture, its model replaced by _TLMaskFeeder (soft target masks of
+    the chunk's references); the module reads its own config.json at import (d = 0.04)."""
+    import importlib
+    tf = types.ModuleType("tensorflow")
+    tf.lite = types.SimpleNamespace(Interpreter=None)
+    sys.modules.setdefault("tensorflow", tf)
+    tl_dir = os.path.join(REF, "rt_av_zoom", "core", "tf_lite_version")
+    cwd = os.getcwd()
+    os.chdir(tl_dir)  # its config.json (read-only use)
+    try:
+        with contextlib.redirect_stdout(open(os.devnull, "w")):
+            tl = importlib.import_module("rt_av_zoom.core.tf_lite_version.inference")
+    finally:
+        os.chdir(cwd)
+    for k, (m, t, i) in trip.items():
+        tf32 = t.astype(np.float32) / 32768.0
+        if32 = i.astype(np.float32) / 32768.0
+        _TLMaskFeeder.masks = chunk_soft_masks(tf32, if32, len(m), chunk=tl.WIN_SIZE,
+                                               hop=tl.WIN_SIZE // 2, n_fft=tl.N_FFT)
+        _TLMaskFeeder.features = []
+        old = tl.TFLiteBeamformer
+        tl.TFLiteBeamformer = _TLMaskFeeder
+        with tempfile.TemporaryDirectory() as td:
+            inp = os.path.join(td, "mixture.wav")
+            wavfile.write(inp, 16000, m)
+            model = os.path.join(td, "absent.tflite")
+            open(model, "wb").close()  # the size print needs a file; the feeder needs none
+            _WRITES.clear()
+            try:
+                with contextlib.redirect_stdout(open(os.devnull, "w")):
+                    tl.process_audio_file(inp, os.path.join(td, "enhanced.wav"), model)
+            finally:
+                tl.TFLiteBeamformer = old
+        out = _WRITES["enhanced.wav"]
+        L = min(len(out), len(tf32))
+        sdr_o, sir_o = run_metrics.calculate_metrics_manual(out[:L], tf32[:L], if32[:L])
+        lm, ipd = _TLMaskFeeder.features[0]
+        save(f"tflite_{k}.npz", chunk=tl.WIN_SIZE, n_fft=tl.N_FFT, hop=tl.HOP, d=tl.D, c=tl.C,
+             sigma=tl.SIGMA, masks=np.stack(_TLMaskFeeder.masks), out=out.astype(np.float32),
+             out_len=len(out), sumsq=np.sum(out ** 2), sir_out=sir_o, sdr_out=sdr_o,
+             chunk0_logmag=lm.astype(np.float32), chunk0_ipd=ipd.astype(np.float32))
+
+
 def main():
     od, mm, run_metrics, metrics = install_reference()
     mpath = os.path.join(HERE, "MANIFEST.json")
@@ -571,6 +648,8 @@ def main():
             gen_world(trip, save)
         if "spectral" in only:
             gen_spectral(trip, save)
+        if "tflite" in only:
+            gen_tflite(trip, run_metrics, save)
         with open(mpath, "w") as fh:
             json.dump(manifest, fh, indent=1, sort_keys=True)
         return
@@ -660,6 +739,7 @@ def main():
     gen_neural(trip, run_metrics, save)
     gen_world(trip, save)
     gen_spectral(trip, save)
+    gen_tflite(trip, run_metrics, save)
 
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)

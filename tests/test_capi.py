@@ -34,7 +34,8 @@ def test_strerror_and_host_side_validation():
     lib = _lib.lib
     assert lib.avz_strerror(0) == b"ok"
     assert lib.avz_strerror(-4) == b"unsupported configuration"
-    assert lib.avz_version() >= 1
+    assert lib.avz_version() == _lib.ABI_VERSION == 2
+    assert b"aligned" in lib.avz_strerror(_lib.AVZ_ERR_ALIGN)
     c = _lib.AvzConfig(fs=16000, n_fft=768, hop=384, sigma=1.0, angle_deg=90.0, mic_d=0.01,
                        c_sound=343.0, fmin_hz=100.0, mask_mode=0, postfilter=1, pf_floor=0.05,
                        weight_eps=0.0, normalize=1, norm_eps=0.0, max_batch=1, max_samples=4096)
@@ -47,6 +48,13 @@ def test_strerror_and_host_side_validation():
     c.postfilter, c.max_samples = 0, 100            # shorter than one frame
     assert lib.avz_plan_create(ct.byref(h), ct.byref(c)) == _lib.AVZ_ERR_ARG
     assert lib.avz_mvdr_batch(None, None, None) == _lib.AVZ_ERR_ARG
+    # scene generator: source Philox streams must stay below the noise streams (0x100 + mic),
+    # and the 0.25-s envelope block must be non-empty; rejected before any device work
+    gen = lambda k, fs: lib.avz_scene_generate(1, 0, k, 16000, 0, 0.01, 343.0, fs, 0.0,  # noqa
+                                               30.0, None, 0, 0, None, None, 0, None, 0, None)
+    assert gen(255, 16000.0) == _lib.AVZ_ERR_ARG
+    assert gen(2, 3.0) == _lib.AVZ_ERR_ARG
+    assert gen(2, float("nan")) == _lib.AVZ_ERR_ARG
 
 
 def test_ctypes_struct_layout_matches_header(tmp_path):

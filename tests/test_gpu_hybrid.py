@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden, triple_f32
+from conftest import golden, hybrid_bin_causes, triple_f32
 from oracle import avz_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -64,31 +64,11 @@ def test_hybrid_weights_vs_oracle(fp, gpu_device):
     Wo = O.hybrid_weights_vec(Y, M, f)
     close = np.abs(Wg - Wo).max(axis=1) <= 1e-3 * np.maximum(1.0, np.abs(Wo).max(axis=1))
     assert (np.abs(Wg[:13] - [1, 0]) == 0).all()
-    # Every bin whose weights differ must be explained: (a) a different noise-frame count
-    # (IBM ties of the fp32 STFT, as in test_gpu_parity), (b) a near-degenerate principal
-    # eigenvector (relative eigen-gap < 1e-4: the direction is ill-conditioned), or (c) the
-    # cond_2 <= cond_max branch decided within 1e-4 of its threshold.
-    Yd = Y.astype(np.complex128)
-    m = (1.0 - M).astype(np.float64)
-    nrm = m.sum(axis=1) + 1e-6
-    a = np.einsum("ft,ft->f", m, np.abs(Yd[0]) ** 2) / nrm
-    e = np.einsum("ft,ft->f", m, np.abs(Yd[1]) ** 2) / nrm
-    b = np.einsum("ft,ft->f", m, Yd[0] * Yd[1].conj()) / nrm
-    gap = 2 * np.sqrt((0.5 * (a - e)) ** 2 + np.abs(b) ** 2) / np.maximum(a + e, 1e-300)
+    # every bin whose weights differ must be explained (conftest.hybrid_bin_causes)
     cnt_gpu = cov[0, :, 4].cpu().numpy()
-    causes = {"mask count": 0, "eigen-gap": 0, "cond branch": 0}
-    for k in np.nonzero(~close)[0]:
-        if cnt_gpu[k] != m[k].sum():
-            causes["mask count"] += 1
-        elif gap[k] < 1e-4:
-            causes["eigen-gap"] += 1
-        else:
-            w_alt = O.hybrid_weights_vec(Y[:, k:k + 1], M[k:k + 1], f[k:k + 1], cond_max=1e300)
-            w_ds = O.hybrid_weights_vec(Y[:, k:k + 1], M[k:k + 1], f[k:k + 1], cond_max=-1.0)
-            flip = any(np.abs(Wg[k] - w[0]).max() <= 1e-3 * max(1.0, np.abs(w[0]).max())
-                       for w in (w_alt, w_ds))
-            assert flip, (k, Wg[k], Wo[k])
-            causes["cond branch"] += 1
+    causes = hybrid_bin_causes(
+        Y, M, f, np.nonzero(~close)[0],
+        lambda k, w: np.abs(Wg[k] - w).max() <= 1e-3 * max(1.0, np.abs(w).max()), cnt=cnt_gpu)
     print(f"hybrid chunk 0: {int((~close).sum())} of {len(close)} bins differ: {causes}")
 
 

@@ -72,27 +72,32 @@ def test_stft_stage(avz, gpu_device, n):
 
 
 # ----------------------------------------------------------------------------- fused IBM
+MAX_IBM_FLIPS = 4      # per golden: measured 0-2 (profiles/r02r/gpu_tests_fidelity.txt)
+IBM_TIE_MARGIN = 1e-7  # fp32 FFT rounding relative to the frame's largest bin; measured <= 1.6e-8
+
+
 def ibm_flip_report(name, cov, st):
     """Mask fidelity of the IBM chain: per-bin noise-frame counts (cov_out column 4) against
     the oracle's (pinned to the reference's stage_* goldens). Counts are exact except where
     |S_int| ~ |S_tgt| to within fp32 FFT rounding (the GPU STFT is fp32; scipy's is fp64
-    rounded to complex64). FFT error scales with the frame's largest bin, so a flipped bin
-    must hold a tie relative to that scale; any other flip fails."""
+    rounded to complex64). FFT error scales with the frame's largest bin, so every flipped
+    (bin, frame) must be a tie relative to that scale: a bin's count may move by at most its
+    number of tie frames (|d| < IBM_TIE_MARGIN of the scale), and a golden holds at most
+    MAX_IBM_FLIPS flips in all."""
     msum = st["mask"].sum(axis=1)
     diff = np.nonzero(cov[:, 4] != msum)[0]
-    assert len(diff) <= max(1, len(msum) // 100)
     frame_scale = np.maximum(np.abs(st["S_i"]).max(axis=0), np.abs(st["S_t"]).max(axis=0))
     margins = []
     for k in diff:
         a, b = np.abs(st["S_i"][k]), np.abs(st["S_t"][k])
         rel = np.abs(a - b) / np.maximum(frame_scale, 1e-30)
+        n_ties = int(np.sum(rel < IBM_TIE_MARGIN))
         margins.append(float(np.min(rel)))
-        assert np.min(rel) < 1e-5, (k, np.min(rel))
-    # mask fidelity: bins whose noise-frame count differs, and how close to a tie the
-    # closest (|S_int| - |S_tgt|) of each was; non-tie flips would have failed above
+        assert abs(cov[k, 4] - msum[k]) <= n_ties, (k, cov[k, 4], msum[k], np.min(rel))
     n_flip = int(np.sum(np.abs(cov[diff, 4] - msum[diff])))
     print(f"{name}: IBM flips {n_flip} in {len(diff)}/{len(msum)} bins "
           f"(all ties; max relative margin {max(margins, default=0.0):.1e}), non-tie flips 0")
+    assert n_flip <= MAX_IBM_FLIPS, n_flip
 
 
 EXC = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "excerpt_*.npz")))
