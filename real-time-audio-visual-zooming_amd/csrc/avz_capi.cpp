@@ -22,6 +22,7 @@ struct Workspace {
   float* heads;
   float* tails;
   uint32_t* peak_u;
+  uint32_t* done;            // [batch] synthesis arrival tickets (fused finalize)
   int* flag;                 // [batch] item-level fallback flags (AVZ_FALLBACK_BATCH)
   float* pf_gain;            // [batch][nchunk][32][F] IRM gains (AVZ_PF_IRM plans only)
 };
@@ -48,10 +49,11 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
     w->heads = reinterpret_cast<float*>(q); q += sz_ht;
     w->tails = reinterpret_cast<float*>(q); q += sz_ht;
     w->peak_u = reinterpret_cast<uint32_t*>(q); q += sz_b;
+    w->done = reinterpret_cast<uint32_t*>(q); q += sz_b;
     w->flag = reinterpret_cast<int*>(q); q += sz_b;
     w->pf_gain = sz_gain ? reinterpret_cast<float*>(q) : nullptr;
   }
-  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 2 * sz_b + sz_gain;
+  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 3 * sz_b + sz_gain;
 }
 
 struct avz_plan {
@@ -318,6 +320,7 @@ static int prepare_chain(const avz_plan* p, const avz_batch_args* a, int use, av
   k.heads = ws.heads;
   k.tails = ws.tails;
   k.peak_u = ws.peak_u;
+  k.done = ws.done;
   k.flag = ws.flag;
   k.pf_gain = ws.pf_gain;
   if (use == USE_COVARIANCE) {  // that stage produces cov_out only: leave the caller's

@@ -42,6 +42,31 @@ namespace avz {
 #ifndef AVZ_SYN_INV2
 #define AVZ_SYN_INV2 1
 #endif
+#ifndef AVZ_SYN_HALF
+#define AVZ_SYN_HALF 0
+#endif
+// The chain's finalize folded into the synthesis kernel: the last chunk item of an
+// utterance to finish (arrival ticket) writes its seams and peak and, for peak
+// normalisation, rescales the utterance in place (fused_finalize).
+#ifndef AVZ_FUSED_FIN
+#define AVZ_FUSED_FIN 0
+#endif
+
+// 16-B write-through (sc1) buffer stores and L1-bypassing (sc1) loads: the hand-off form of
+// MI355X_MICROARCH's inter-workgroup table (stores all sc1, every storing wave's vmcnt
+// drained before one lane's agent-scope atomic add, the last adder reads with sc1 loads).
+constexpr int kSC1 = 16;  // buffer-op cache policy bit: sc1 (gfx940+)
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st4_sc1(rsrc_t r, int elem, float4 v) {
+  const v4i_t d = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z),
+                   __float_as_int(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(d, r, elem * 4, 0, kSC1);
+}
+__device__ __forceinline__ float4 ld4_sc1(rsrc_t r, int elem) {
+  const v4i_t d = __builtin_amdgcn_raw_buffer_load_b128(r, elem * 4, 0, kSC1);
+  return make_float4(__int_as_float(d.x), __int_as_float(d.y), __int_as_float(d.z),
+                     __int_as_float(d.w));
+}
 
 constexpr int kChunk = 32;      // frames per chunk = bits of one mask word
 constexpr int kCThreads = 256;  // 4 waves
@@ -283,6 +308,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   if (c >= nch) return;
   if (c == 0 && tid == 0) {
     A.peak_u[b] = 0u;
+    if (A.done) A.done[b] = 0u;  // the synthesis kernel's arrival tickets
     if (A.peak && A.normalize != NORM_PEAK) A.peak[b] = 0.0f;  // finalize's atomicMax target
   }
   const int t0 = c * kChunk;
@@ -352,9 +378,14 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   float* const gain = IRM ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F : nullptr;
   // Nyquist bin N/2: frame `lane` of each step on the last wave's lanes.
   const bool nyq_wave = (wave == G::NWAVE - 1);
-  Acc32 an;
+  Acc32 an, adc;  // Nyquist; DC (IPD: weighed on the Nyquist wave, not by lane 0)
   an.zero();
+  adc.zero();
   uint32_t nyq_bits = 0u;
+  // IPD: covariance weight of the main bin loop, 0 on the DC lane (bin tid + 256 j)
+  float wone[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) wone[j] = (MASK == MASK_IPD && j == 0 && tid == 0) ? 0.0f : 1.0f;
 
   AVZ_STAMP_DECL();
   issue_loads(0);
@@ -453,13 +484,27 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
               split_pair2(zm[i], zmp[i], x0, x1);  // 2 y0, 2 y1
               if constexpr (MASK == MASK_IPD) {
                 // the exact angle test of near-colinear bins runs after the loop
+#if AVZ_BINS_V1
                 const bool clear = ipd_clear(x0, x1) && !((ident_w >> (8 * (g0 + i))) & 1ull);
                 ipd_fix[j] |= (clear ? 0u : 1u) << (g0 + i);
-#if AVZ_BINS_V1
                 const float w = clear ? 1.0f : 0.0f;
                 acc[j].add(x0, x1, w, w);
 #else
-                acc[j].add_sel(x0, x1, clear);  // weight count: nclear below
+                // ipd_clear on the covariance products themselves: |x0|^2 |x1|^2 and
+                // Im x0 conj(x1) are the test's norm and cross product. Every frame's
+                // products go in at weight 1 (wone: 0 on the DC lane, weighed by the Nyquist
+                // wave); the frames the test leaves open get w - 1 after the loop.
+                const float p0 = x0.x * x0.x + x0.y * x0.y;
+                const float p1 = x1.x * x1.x + x1.y * x1.y;
+                const float re = x0.x * x1.x + x0.y * x1.y;
+                const float im = x0.y * x1.x - x0.x * x1.y;
+                const bool clear = im * im > 1e-10f * (p0 * p1) &&
+                                   !((ident_w >> (8 * (g0 + i))) & 1ull);
+                ipd_fix[j] |= (clear ? 0u : 1u) << (g0 + i);
+                acc[j].c00 = fmaf(wone[j], p0, acc[j].c00);
+                acc[j].c11 = fmaf(wone[j], p1, acc[j].c11);
+                acc[j].c01r = fmaf(wone[j], re, acc[j].c01r);
+                acc[j].c01i = fmaf(wone[j], im, acc[j].c01i);
 #endif
                 continue;
               }
@@ -506,15 +551,17 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
       bin_phase(std::false_type{}, std::false_type{});
     }
     if constexpr (MASK == MASK_IPD) {
-      // Near-colinear (bin, frame) pairs (always DC, rarely any other): exact weight from
-      // the spectra still in LDS. Waves with no such lane skip this.
+      // Near-colinear (bin, frame) pairs (rare; DC, always one, is the Nyquist wave's):
+      // exact weight from the spectra still in LDS. Waves with no such lane skip this.
 #pragma unroll
       for (int j = 0; j < BPT; ++j) {
         const int kb = tid + j * NT;
         const int kp = (N - kb) & (N - 1);
         uint32_t f = ipd_fix[j];
 #if !AVZ_BINS_V1
-        ipd_clear_n[j] += nvalid - __popc(f);  // frames weighted 1 by add_sel
+        const bool dc = (j == 0 && tid == 0);
+        if (dc) f = 0u;
+        ipd_clear_n[j] += dc ? 0 : nvalid - __popc(f);  // weight count: exact integers
 #endif
         while (f) {
           const int i = __builtin_ctz(f);
@@ -523,7 +570,11 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
           cf x0, x1;
           split_pair2(Zm[kb], Zm[kp], x0, x1);
           const float w = ((ident_w >> (8 * i)) & 1ull) ? 0.01f : ipd_weight_exact(x0, x1);
+#if AVZ_BINS_V1
           acc[j].add(x0, x1, w, w);
+#else
+          acc[j].add(x0, x1, w - 1.0f, w);  // the products went in at weight 1
+#endif
         }
       }
     }
@@ -538,6 +589,13 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         float mn = bin_mask<MASK>(A, b, y0, y1, zr, zr, N / 2, f0 + lane, noise, wn);
         if (MASK == MASK_IPD && ((ident_w >> (8 * lane)) & 1ull)) wn = mn = 0.01f;
         an.add(y0, y1, wn, mn);
+        if constexpr (MASK == MASK_IPD && !AVZ_BINS_V1) {  // DC of frame `lane`
+          cf d0, d1;
+          const cf z0 = Zm[0];
+          split_pair2(z0, z0, d0, d1);
+          const float wd = ((ident_w >> (8 * lane)) & 1ull) ? 0.01f : ipd_weight_exact(d0, d1);
+          adc.add(d0, d1, wd, wd);
+        }
         if constexpr (IRM) gain[(step * FB + lane) * F + N / 2] = irm_gain(zr, zr);
       }
       const unsigned long long bal = __ballot(noise);
@@ -551,9 +609,11 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   // ---- chunk partials
   float* P = A.part + ((long long)b * A.nchunk + c) * 5 * F;
   uint32_t* MW = A.mwords + ((long long)b * A.nchunk + c) * F;
+  constexpr bool DC_NYQ = MASK == MASK_IPD && !AVZ_BINS_V1;  // DC sums come from the Nyquist wave
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
     const int kb = tid + j * NT;
+    if (DC_NYQ && kb == 0) continue;
 #if !AVZ_BINS_V1
     // binary weights were folded into the selects: their count is exact in fp32
     if constexpr (MASK == MASK_IBM) acc[j].cm = (float)__popc(bits[j]);
@@ -573,6 +633,20 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
       an.c01r += __shfl_xor(an.c01r, o, 64);
       an.c01i += __shfl_xor(an.c01i, o, 64);
       an.cm += __shfl_xor(an.cm, o, 64);
+      if constexpr (DC_NYQ) {
+        adc.c00 += __shfl_xor(adc.c00, o, 64);
+        adc.c11 += __shfl_xor(adc.c11, o, 64);
+        adc.c01r += __shfl_xor(adc.c01r, o, 64);
+        adc.c01i += __shfl_xor(adc.c01i, o, 64);
+        adc.cm += __shfl_xor(adc.cm, o, 64);
+      }
+    }
+    if (DC_NYQ && lane == 0) {
+      P[0 * F] = adc.c00;
+      P[1 * F] = adc.c11;
+      P[2 * F] = adc.c01r;
+      P[3 * F] = adc.c01i;
+      P[4 * F] = adc.cm;
     }
     if (lane == 0) {
       P[0 * F + N / 2] = an.c00;
@@ -742,7 +816,10 @@ __global__ void __launch_bounds__(kSrpThreads) avz_srp_kernel(ChainArgs A, SrpAr
 // ================================ synthesis ================================
 // SPEC: the frames' spectra come from A.spec (avz_istft: scipy.signal.istft of a given
 // S[b][k][t]) instead of the forward FFT of the mixture and the apply step.
-template <int N, int PF, bool SPEC>
+template <int N>
+__device__ void fused_finalize(const ChainArgs& A, int b, int T, int nch, float* red);
+
+template <int N, int PF, bool SPEC, bool FUSED>
 __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char* lds, int c,
                                                int b) {
   static_assert(!SPEC || PF == PF_NONE, "spectrum input carries its own post-filter");
@@ -755,8 +832,12 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   constexpr int NSG = NT / M4;        // segment groups
   constexpr int SPT = FB / NSG;       // segments per thread per step
   static_assert(SPT * NSG == FB, "OLA mapping");
-  // N = 1024 inverse as two x2 transforms on waves 0-1 instead of four 64-lane x1 ones
-  constexpr bool INV2 = N == 1024 && !AVZ_X1 && AVZ_SYN_INV2;
+  // N = 1024 inverse, one real frame per N/2-point complex transform (HALF): every wave
+  // runs one Fft512x2 pair (frames 2w, 2w + 1 in their own slots), instead of two packed
+  // frames per 1024-point transform on waves 0-1 while waves 2-3 wait at the barrier
+  // (INV2) or four 64-lane x1 transforms. The spectrum input path (SPEC) keeps INV2.
+  constexpr bool HALF = N == 1024 && !AVZ_X1 && AVZ_SYN_HALF && !SPEC;
+  constexpr bool INV2 = N == 1024 && !AVZ_X1 && AVZ_SYN_INV2 && !HALF;
 
   cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
   float* red = reinterpret_cast<float*>(lds + G::MISC_OFF);
@@ -764,12 +845,19 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
   const int L = utt_len(A, b);
-  if (L < N) return;
+  if (L < N) {  // host validates; a bad device length reports NaN
+    if (FUSED && c == 0 && tid == 0 && A.peak) A.peak[b] = __builtin_nanf("");
+    return;
+  }
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
   if (c >= nch) return;
   const int t0 = c * kChunk;
   const int nstep = (min(kChunk, T - t0) + FB - 1) / FB;
+  // FUSED: everything the utterance's last item reads back is stored write-through
+  const rsrc_t r_out = make_rsrc(A.out + (long long)b * A.out_stride, (long long)(T - 1) * H);
+  const rsrc_t r_heads = make_rsrc(A.heads + (long long)b * A.nchunk * H, (long long)A.nchunk * H);
+  const rsrc_t r_tails = make_rsrc(A.tails + (long long)b * A.nchunk * H, (long long)A.nchunk * H);
 
   typename C::Fft fft;
   fft.init(lane);
@@ -801,19 +889,30 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   AVZ_STAMP_INIT();
   if constexpr (!SPEC) issue_loads(0);
 
-  // ---- apply coefficients and post-filter bits of this thread's bins
+  // ---- apply coefficients and post-filter bits of this thread's bins: tid + 256 j, or
+  // (HALF) the pair tid, N/2 - tid whose spectra meet in bin tid of the N/2-point inverse
   const float4* coef = reinterpret_cast<const float4*>(A.coef) + (long long)b * F;
   const uint32_t* MW = A.mwords + ((long long)b * A.nchunk + c) * F;
+  auto bin_of = [&](int j) { return HALF ? (j == 0 ? tid : H - tid) : tid + j * NT; };
   cf alpha[BPT], beta[BPT];
   uint32_t bits[BPT];
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
-    const float4 cw = SPEC ? make_float4(0.f, 0.f, 0.f, 0.f) : coef[tid + j * NT];
+    const float4 cw = SPEC ? make_float4(0.f, 0.f, 0.f, 0.f) : coef[bin_of(j)];
     alpha[j] = cf{cw.x, cw.y};
     beta[j] = cf{cw.z, cw.w};
-    bits[j] = (PF == PF_IBM_TARGET) ? MW[tid + j * NT] : 0u;
+    bits[j] = (PF == PF_IBM_TARGET) ? MW[bin_of(j)] : 0u;
+  }
+  // HALF: e^{+2 pi i tid / N}, the odd-sample twiddle of the bin pair
+  cf om{1.0f, 0.0f};
+  if constexpr (HALF) {
+    double sn, cs;
+    sincospi(2.0 * tid / N, &sn, &cs);
+    om = cf{(float)cs, (float)sn};
   }
   const bool nyq_wave = (wave == G::NWAVE - 1);
+  // the one bin outside the pairs: N/2 (Nyquist) or, HALF, N/4 (its own partner)
+  constexpr int KN = HALF ? N / 4 : N / 2;
   cf alpha_n{0, 0}, beta_n{0, 0};
   uint32_t bits_n = 0u;
   // spectrum input: S[b][k][t] rows (t contiguous); frames past spec_frames read as zero
@@ -823,10 +922,10 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   const bool svec = SPEC && ((A.spec_sb | A.spec_sf) & 1) == 0 &&
                     ((reinterpret_cast<uintptr_t>(A.spec) & 15) == 0);
   if (nyq_wave && !SPEC) {
-    const float4 cw = coef[N / 2];
+    const float4 cw = coef[KN];
     alpha_n = cf{cw.x, cw.y};
     beta_n = cf{cw.z, cw.w};
-    if (PF == PF_IBM_TARGET) bits_n = MW[N / 2];
+    if (PF == PF_IBM_TARGET) bits_n = MW[KN];
   }
   const float* irm = (PF == PF_IRM) ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F
                                     : nullptr;
@@ -859,7 +958,17 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   float peak = 0.0f;
   const bool ifft_wave = wave < NPAIR / C::FPW;  // waves holding a pair (x2 inverse)
   float wi_c = 0.f, wi_s = 0.f;  // N = 1024 inverse: 0.25 cos / sin(2 pi n0 / N), x1 layout
-  if constexpr (N == 1024) {
+  // HALF: samples 2 m, 2 m + 1 of the Fft512x2 output m = (lane & 15) + 256 h + 16 k
+  float wh_c[2] = {0.f, 0.f}, wh_s[2] = {0.f, 0.f};
+  if constexpr (HALF) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      double sn, cs;
+      sincospi(2.0 * (2 * ((lane & 15) + 256 * ((lane >> 4) & 1)) + e) / N, &sn, &cs);
+      wh_c[e] = (float)(0.25 * cs);
+      wh_s[e] = (float)(0.25 * sn);
+    }
+  } else if constexpr (N == 1024) {
     double sn, cs;
     sincospi(2.0 * ((lane & 31) + 512 * (lane >> 5)) / N, &sn, &cs);
     wi_c = (float)(0.25 * cs);
@@ -944,6 +1053,75 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       }
     }
     };
+    // HALF: per frame f (slot f) the spectra S[k], S[N/2 - k] of the thread's pair
+    // k = tid give the N/2-point inverse's input at both (x[n] = sum_k S^[k] e^{2 pi i k n/N}
+    // split into even / odd samples, z[m] = x[2m] + i x[2m+1]):
+    //   Zh[k] = A + i B,  Zh[N/2 - k] = conj(A) + i conj(B),
+    //   A = S[k] + conj(S[N/2 - k]),  B = e^{2 pi i k / N} (S[k] - conj(S[N/2 - k])).
+    // Written in place over the bins just read (no other thread reads them). tid 0 pairs
+    // DC with Nyquist (real parts only, as irfft); its second write lands on bin N/2,
+    // which only it reads and the inverse does not. Bin N/4 (its own partner) is done
+    // below by the Nyquist wave.
+    auto apply_half = [&](auto vec) {
+      constexpr bool VEC = decltype(vec)::value;
+      const int kA = tid, kB = H - tid;
+      float gv[2][VEC ? FB : 1];
+      if constexpr (VEC) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float4* mp = reinterpret_cast<const float4*>(
+              A.ext_mask + (long long)b * A.mask_sb + (long long)bin_of(j) * A.mask_sf + f0);
+#pragma unroll
+          for (int q = 0; q < FB / 4; ++q) {
+            const float4 m = mp[q];
+            gv[j][4 * q + 0] = m.x;
+            gv[j][4 * q + 1] = m.y;
+            gv[j][4 * q + 2] = m.z;
+            gv[j][4 * q + 3] = m.w;
+          }
+#pragma unroll
+          for (int i = 0; i < FB; ++i)
+            if constexpr (PF == PF_EXT_FLOOR) gv[j][i] = fmaxf(gv[j][i], A.pf_floor);
+        }
+      }
+      constexpr int GF = 4;  // frames whose reads are issued together
+#pragma unroll
+      for (int f = 0; f < FB; f += GF) {
+        cf za[GF], zap[GF], zb[GF], zbp[GF];
+#pragma unroll
+        for (int i = 0; i < GF; ++i) {
+          const cf* Z = slot_ptr<N>(lds, f + i);
+          za[i] = lds_read(Z + kA);
+          zap[i] = lds_read(Z + ((N - kA) & (N - 1)));
+          zb[i] = lds_read(Z + kB);
+          zbp[i] = lds_read(Z + (N - kB));
+        }
+#pragma unroll
+        for (int i = 0; i < GF; ++i) {
+          const int t = f0 + f + i, ib = step * FB + f + i;
+          float ga, gb;
+          if constexpr (VEC) {
+            ga = gv[0][f + i];
+            gb = gv[1][f + i];
+          } else {
+            ga = gain(bits[0], ib, t, kA);
+            gb = gain(bits[1], ib, t, kB);
+          }
+          cf sa = apply_bin(alpha[0], beta[0], za[i], zap[i], ga);
+          cf sb = apply_bin(alpha[1], beta[1], zb[i], zbp[i], gb);
+          if (tid == 0) {  // DC and Nyquist: irfft keeps the real parts
+            sa.y = 0.0f;
+            sb.y = 0.0f;
+          }
+          const cf a = {sa.x + sb.x, sa.y - sb.y};  // S[k] + conj S[N/2 - k]
+          const cf d = {sa.x - sb.x, sa.y + sb.y};  // S[k] - conj S[N/2 - k]
+          const cf bb = c_mul(om, d);
+          cf* Z = slot_ptr<N>(lds, f + i);
+          Z[kA] = {a.x - bb.y, a.y + bb.x};
+          Z[kB] = {a.x + bb.y, bb.x - a.y};
+        }
+      }
+    };
     // spectrum input: the step's frames of the thread's bins straight from S, packed as
     // above (16-B row segments when the rows are aligned and the step is complete)
     auto spec_phase = [&](auto vec) {
@@ -981,6 +1159,11 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         spec_phase(std::true_type{});
       else
         spec_phase(std::false_type{});
+    } else if constexpr (HALF) {
+      if ((PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) && mask_vec && f0 + FB <= T)  // block-uniform
+        apply_half(std::true_type{});
+      else
+        apply_half(std::false_type{});
     } else if constexpr (PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) {
       if (mask_vec && f0 + FB <= T)  // wave-uniform
         apply_phase(std::true_type{});
@@ -997,7 +1180,14 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         slot_ptr<N>(lds, 2 * lane)[N / 2] = {xa, xb};
       }
     }
-    if (!SPEC && nyq_wave && lane < NPAIR) {  // Nyquist bin: frame pair `lane`
+    if (HALF && nyq_wave && lane < FB) {  // bin N/4 of frame `lane`: Zh = 2 conj(S)
+      const int t = f0 + lane;
+      cf* Z = slot_ptr<N>(lds, lane);
+      const float g = gain(bits_n, step * FB + lane, t, N / 4);
+      const cf s = apply_bin(alpha_n, beta_n, Z[N / 4], Z[3 * N / 4], g);
+      Z[N / 4] = {2.0f * s.x, -2.0f * s.y};
+    }
+    if (!HALF && !SPEC && nyq_wave && lane < NPAIR) {  // Nyquist bin: frame pair `lane`
       const int ta = f0 + 2 * lane;
       if (ta < T) {
         const int ia = step * FB + 2 * lane;
@@ -1013,7 +1203,22 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     AVZ_STAMP(7);
 
     // ---- inverse FFT of the packed pairs -> windowed frame contributions in slot 2p+1
-    if constexpr (N == 1024 && AVZ_X1) {
+    //      (HALF: of each frame's N/2-point input -> its own slot)
+    if constexpr (HALF) {
+      cf u[16];
+      cf* Zi = slot_ptr<N>(lds, my_slot);
+      static_for<0, 16>([&](auto r) { u[r] = c_conj(lds_read(Zi + (lane & 31) + 32 * r)); });
+      Fft512x2::forward_tw1024(u, Zi + H, twid, lane);
+      // u[k] = conj(z[m]), m = (lane & 15) + 16 k + 256 h: samples 2m (Re z), 2m + 1 (Im z)
+      float2* Cp = reinterpret_cast<float2*>(Zi);
+      const int mh = (lane & 15) + 256 * ((lane >> 4) & 1);
+      static_for<0, 16>([&](auto k) {
+        constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi (32 k) / N
+        const float we = fmaf(wh_s[0], sk, fmaf(-wh_c[0], ck, 0.25f));
+        const float wo = fmaf(wh_s[1], sk, fmaf(-wh_c[1], ck, 0.25f));
+        Cp[mh + 16 * k] = make_float2(u[k].x * we, -u[k].y * wo);
+      });
+    } else if constexpr (N == 1024 && AVZ_X1) {
       // two pairs: waves 0-1 run one 64-lane 1024-point transform each (register twiddles;
       // output register k of lane (l, h) is sample l + 512 h + 32 k)
       if (wave < NPAIR) {
@@ -1081,6 +1286,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
 
     // ---- overlap-add: segment j = f0 - 1 + s = frame s-1 (2nd half) + frame s (1st half)
     auto cframe = [&](int f) -> const float* {
+      if constexpr (HALF) return reinterpret_cast<const float*>(slot_ptr<N>(lds, f));
       return reinterpret_cast<const float*>(slot_ptr<N>(lds, 2 * (f >> 1) + 1)) + (f & 1) * N;
     };
 #pragma unroll
@@ -1088,7 +1294,10 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       const int s = sgrp + si * NSG;
       const float4 vb = *reinterpret_cast<const float4*>(cframe(s) + m0);
       if (s == 0 && step == 0) {  // chunk's first frame: finalize adds the previous tail
-        *reinterpret_cast<float4*>(A.heads + ((long long)b * A.nchunk + c) * H + m0) = vb;
+        if constexpr (FUSED)
+          st4_sc1(r_heads, c * H + m0, vb);
+        else
+          *reinterpret_cast<float4*>(A.heads + ((long long)b * A.nchunk + c) * H + m0) = vb;
         continue;
       }
       const int j = f0 - 1 + s;
@@ -1100,7 +1309,10 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         o.y = (va.y + vb.y) * inv[1];
         o.z = (va.z + vb.z) * inv[2];
         o.w = (va.w + vb.w) * inv[3];
-        *reinterpret_cast<float4*>(outb + (long long)j * H + m0) = o;
+        if constexpr (FUSED)
+          st4_sc1(r_out, j * H + m0, o);
+        else
+          *reinterpret_cast<float4*>(outb + (long long)j * H + m0) = o;
         peak = fmaxf(peak, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
       }
     }
@@ -1108,24 +1320,39 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     lds_barrier();
     AVZ_STAMP(9);
   }
-  if (sgrp == 0 && nstep * FB == kChunk)  // full chunk: its last frame's tail
-    *reinterpret_cast<float4*>(A.tails + ((long long)b * A.nchunk + c) * H + m0) = carry;
+  if (sgrp == 0 && nstep * FB == kChunk) {  // full chunk: its last frame's tail
+    if constexpr (FUSED)
+      st4_sc1(r_tails, c * H + m0, carry);
+    else
+      *reinterpret_cast<float4*>(A.tails + ((long long)b * A.nchunk + c) * H + m0) = carry;
+  }
 
   // ---- block max |out| -> utterance running max (non-negative floats order as uints)
   for (int o = 32; o > 0; o >>= 1) peak = fmaxf(peak, __shfl_xor(peak, o, 64));
   if (lane == 0) red[wave] = peak;
+  if constexpr (FUSED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores
   __syncthreads();
   if (tid == 0) {
     float pk = red[0];
 #pragma unroll
     for (int w = 1; w < G::NWAVE; ++w) pk = fmaxf(pk, red[w]);
     atomicMax(A.peak_u + b, __float_as_uint(pk));
+    if constexpr (FUSED) {  // arrival ticket, behind the block's drained stores and its max
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t t = atomicAdd(A.done + b, 1u);
+      reinterpret_cast<int*>(red)[G::NWAVE] = (t + 1u == (uint32_t)nch) ? 1 : 0;
+    }
+  }
+  if constexpr (FUSED) {
+    __syncthreads();
+    if (reinterpret_cast<const int*>(red)[G::NWAVE]) fused_finalize<N>(A, b, T, nch, red);
+    __syncthreads();
   }
   AVZ_STAMP(10);
 }
 
 // Persistent grid over (chunk, utterance) items, as avz_analysis_kernel.
-template <int N, int PF, bool SPEC = false>
+template <int N, int PF, bool SPEC = false, bool FUSED = false>
 __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_synthesis_kernel(ChainArgs A) {
   using G = CGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -1133,7 +1360,71 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_syn
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
   const int n_items = gx * A.batch;
   for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-    synthesis_item<N, PF, SPEC>(A, lds, it % gx, it / gx);
+    synthesis_item<N, PF, SPEC, FUSED>(A, lds, it % gx, it / gx);
+}
+
+// Finalize of utterance b inside the synthesis kernel, run by the block whose item was the
+// utterance's last to arrive (every other item's interior, head and tail stores are
+// write-through and drained before its ticket): seams 32 cc - 1 = tails[cc - 1] + heads[cc]
+// (cc = 1 .. nch - 1), the utterance peak (interiors' atomicMax and the seams), peak[b];
+// NORM_PEAK also rescales every interior segment in place (L1-bypassing loads). The same
+// arithmetic as avz_finalize_kernel.
+template <int N>
+__device__ void fused_finalize(const ChainArgs& A, int b, int T, int nch, float* red) {
+  constexpr int NT = kCThreads, H = N / 2, H4 = H / 4, NWAVE = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* outb = A.out + (long long)b * A.out_stride;
+  const rsrc_t r_h = make_rsrc(A.heads + (long long)b * A.nchunk * H, (long long)A.nchunk * H);
+  const rsrc_t r_t = make_rsrc(A.tails + (long long)b * A.nchunk * H, (long long)A.nchunk * H);
+  const rsrc_t r_o = make_rsrc(outb, (long long)(T - 1) * H);
+  const int nseam4 = (nch - 1) * H4;
+  auto seam4 = [&](int idx) -> float4 {  // float4 group idx of the seams, in segment order
+    const int cc = idx / H4 + 1, m = 4 * (idx % H4);
+    const float4 t = ld4_sc1(r_t, (cc - 1) * H + m);
+    const float4 h = ld4_sc1(r_h, cc * H + m);
+    return make_float4((t.x + h.x) * inv_wsum<N>(m), (t.y + h.y) * inv_wsum<N>(m + 1),
+                       (t.z + h.z) * inv_wsum<N>(m + 2), (t.w + h.w) * inv_wsum<N>(m + 3));
+  };
+  float pk = 0.0f;
+  for (int idx = tid; idx < nseam4; idx += NT) {
+    const float4 x = seam4(idx);
+    pk = fmaxf(pk, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+  }
+  for (int o = 32; o > 0; o >>= 1) pk = fmaxf(pk, __shfl_xor(pk, o, 64));
+  if (lane == 0) red[wave] = pk;
+  __syncthreads();
+  pk = __uint_as_float(__hip_atomic_load(A.peak_u + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+  for (int w = 0; w < NWAVE; ++w) pk = fmaxf(pk, red[w]);
+  if (tid == 0 && A.peak) A.peak[b] = pk;
+  const bool norm = A.normalize == NORM_PEAK;
+  const float scale = norm ? 1.0f / (pk + A.norm_eps) : 1.0f;
+  for (int idx = tid; idx < nseam4; idx += NT) {
+    float4 x = seam4(idx);
+    x.x *= scale; x.y *= scale; x.z *= scale; x.w *= scale;
+    const int cc = idx / H4 + 1, m = 4 * (idx % H4);
+    *reinterpret_cast<float4*>(outb + (long long)(kChunk * cc - 1) * H + m) = x;
+  }
+  if (!norm) return;
+  // interior segments j < T - 1, j % 32 != 31 (the seams, written above): 16 loads in
+  // flight per lane, issued unconditionally (the descriptor returns 0 past the end; seam
+  // positions are loaded and dropped) so they are not serialised behind branches
+  constexpr int U = 16;
+  const int n4 = (T - 1) * H4;
+  float4* o4 = reinterpret_cast<float4*>(outb);
+  for (int base = 0; base < n4; base += U * NT) {
+    float4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = ld4_sc1(r_o, 4 * (base + u * NT + tid));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * NT + tid;
+      if (i < n4 && (i / H4) % kChunk != kChunk - 1) {
+        x[u].x *= scale; x[u].y *= scale; x[u].z *= scale; x[u].w *= scale;
+        o4[i] = x[u];
+      }
+    }
+  }
 }
 
 // ================================ finalize ================================
@@ -1233,14 +1524,15 @@ extern "C" int avz_chunk_frames(void) { return kChunk; }
 static int resident_cus();
 
 // The synthesis launch of the chain and of the stage exports (persistent grid).
-template <int N, int PF>
+template <int N, int PF, bool FUSED = false>
 static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   constexpr int lds = CGeo<N>::LDS_BYTES;
-  if (!lds_ready<avz_synthesis_kernel<N, PF>>(lds)) return -3;
+  if (!lds_ready<avz_synthesis_kernel<N, PF, false, FUSED>>(lds)) return -3;
   const int n_items = nch * a->batch;
   const dim3 sgrid((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus()));
-  hipExtLaunchKernelGGL(avz_synthesis_kernel<N, PF>, sgrid, dim3(kCThreads), lds, st, e0, e1, 0, *a);
+  hipExtLaunchKernelGGL((avz_synthesis_kernel<N, PF, false, FUSED>), sgrid, dim3(kCThreads), lds,
+                        st, e0, e1, 0, *a);
   return 0;
 }
 
@@ -1292,8 +1584,17 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   } else {
     hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), evt(3), 0, *a);
   }
+#if AVZ_FUSED_FIN
+  (void)k3;
+  (void)grid;
+  if (launch_synthesis<N, PF, true>(a, st, evt(4), evt(5)) != 0) return -3;
+  if (evt(6) && (hipEventRecord(evt(6), st) != hipSuccess ||  // finalize: fused (0 ms)
+                 hipEventRecord(evt(7), st) != hipSuccess))
+    return -3;
+#else
   if (launch_synthesis<N, PF>(a, st, evt(4), evt(5)) != 0) return -3;
   hipExtLaunchKernelGGL(k3, grid, dim3(kCThreads), 0, st, evt(6), evt(7), 0, *a);
+#endif
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -118,8 +118,16 @@ struct KCfg<512> {
   static constexpr int IN_STRIDE = 32;
   static constexpr int OUT_STRIDE = 16;
   static constexpr int TW_BYTES = 0;
+#ifdef AVZ_B512
+  static constexpr int BLOCKS_PER_CU = AVZ_B512;
+#else
   static constexpr int BLOCKS_PER_CU = 2;
+#endif
+#ifdef AVZ_SB512
+  static constexpr int SYN_BLOCKS_PER_CU = AVZ_SB512;
+#else
   static constexpr int SYN_BLOCKS_PER_CU = 2;
+#endif
 };
 
 template <int N, int NT>

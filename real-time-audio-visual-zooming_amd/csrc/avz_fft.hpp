@@ -509,6 +509,31 @@ struct Fft512x2 {
     dft16(v);
     xhalf_dit<16>(v, sgn);
   }
+
+  // The same transform for a lane that did not init(), with its W512 twiddles read from
+  // Fft1024x2's block table tw[k1 * 32 + l] = W1024^{l k1}: W512^{j i} = tw[2 i][j],
+  // W512^{4 j i} = tw[8 i][j] (the 1024-point synthesis runs its inverse at N/2).
+  __device__ __forceinline__ static void forward_tw1024(cf (&v)[16], cf* scratch, const cf* tw,
+                                                        int lane) {
+    const int jj = lane & 31, kk = lane & 15, hh = (lane >> 4) & 1;
+    const float sg = hh ? -1.0f : 1.0f;
+    cf p[4], q[4];
+    static_for<0, 4>([&](auto i) {
+      p[i] = lds_read(tw + (2 * i) * 32 + jj);
+      q[i] = lds_read(tw + (8 * i) * 32 + jj);
+    });
+    dft16(v);
+    static_for<1, 16>([&](auto k) {
+      const cf t = ((k & 3) == 0) ? q[k >> 2] : c_mul(p[k & 3], q[k >> 2]);
+      v[k] = c_mul(v[k], t);
+    });
+    static_for<0, 16>([&](auto k) { scratch[k * 34 + jj] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = scratch[kk * 34 + 2 * r + hh]; });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<16>(v, sg);
+  }
 };
 
 }  // namespace avz

@@ -44,6 +44,7 @@ struct ChainArgs {
   float* heads;               // [B][nchunk][H] chunk's first frame, first-half contribution
   float* tails;               // [B][nchunk][H] chunk's last frame, second-half contribution
   uint32_t* peak_u;           // [B] max |out| over chunk interiors (float bits, atomicMax)
+  uint32_t* done;             // [B] synthesis items finished (fused finalize's arrival ticket)
   float* pf_gain;             // [B][nchunk][32][F] IRM post-filter gain (PF_IRM) or null
   int singular_fallback;      // 0: w = [1, 0]; 1: w = [1/2, 1/2]
   // spectrum-input synthesis (avz_istft): S[b][k][t] complex64 replaces the forward FFT of
