@@ -303,6 +303,36 @@ def setup_chain4(spec, dev, batches):
     return step, info
 
 
+# avz_beamform_spectral (batch_mvdr on a held STFT, tf_lite_version/inference.py:85-179, with
+# the driver's S * max(M, 0.05) fused): Y 2 x 8 B + mask 4 B read, S 8 B written per TF-bin
+SPECTRAL_BYTES_PER_BIN = 28
+
+
+def setup_spectral(n_items, dev, n_sets):
+    """avz_beamform_spectral over n_items 2-s chunk spectra ([2, 513, 64] complex64 Y, a
+    [513, 64] target mask) per step, the steps alternating over n_sets input sets."""
+    import torch
+
+    from avz import spectral
+    F, T = 513, 64
+    sb = spectral.SpectralBeamformer("mvdr", max_items=n_items, floor=0.05)
+    g = torch.Generator(device=dev).manual_seed(11)
+    sets = []
+    for _ in range(n_sets):
+        Y = torch.view_as_complex(torch.randn((n_items, 2, F, T, 2), generator=g, device=dev))
+        M = torch.rand((n_items, F, T), generator=g, device=dev)
+        sets.append((Y, M, torch.empty((n_items, F, T), dtype=torch.complex64, device=dev)))
+    it = [0]
+
+    def step():
+        Y, M, S = sets[it[0] % len(sets)]
+        it[0] += 1
+        sb.beamform(Y, M, S=S)
+
+    return step, dict(plan=sb.plan, bins=n_items * F * T, it=it,
+                      kernel="avz_spectral_kernel<1024,MVDR,EXT_FLOOR> (+ batch-fallback fixup)")
+
+
 def run_timed(step, plan, K, W, world, dev, settle_on, kernel_timing):
     """Clock settling, W warmup steps, K timed steps (barrier + synchronize on both sides),
     then an untimed pass with HIP events around all four kernels."""
@@ -606,6 +636,27 @@ def main():
             ("configs[4]_chain", dict(workload="chain4", B=1024, k=2, n_fft=1024, normalize="none",
                                       text=WORKLOAD_TEXT["chain4"].format(B=1024, n=1024, h=512))),
         ]
+        try:  # the spectral-domain operator on a 4096-item chunk batch (configs[4]'s items)
+            st, inf = setup_spectral(4096, dev, n_sets)
+            el, _, _ = run_timed(st, inf["plan"], K, args.warmup, 1, dev, not args.no_settle,
+                                 False)
+            v = inf["bins"] * K / el
+            ach = inf["bins"] * SPECTRAL_BYTES_PER_BIN / (el / K) / 1e9
+            secondary["spectral_4096"] = {
+                "config": "avz_beamform_spectral: 4096 items of [2, 513, 64] complex64 STFT + "
+                          "[513, 64] target mask, batch_mvdr semantics (sigma 1e-5, d 0.04, "
+                          "item-level singular fallback), S * max(M, 0.05) fused",
+                "value": v, "unit": "TF-bins/s", "ms_per_step": 1e3 * el / K,
+                "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                             "bytes_per_bin": SPECTRAL_BYTES_PER_BIN,
+                             "alg_bytes_per_launch": inf["bins"] * SPECTRAL_BYTES_PER_BIN,
+                             "kernel": inf["kernel"],
+                             "note": "step wall time / K (both launches of the call)"}}
+            del st, inf
+            torch.cuda.empty_cache()
+        except Exception as exc:  # a side figure must never sink the bench line
+            secondary["spectral_4096"] = {"error": repr(exc)[:300]}
         for name, sp in specs:
             try:
                 bs = [gen_batch(sp, dev, i * sp["B"], args.scenes) for i in range(n_sets)]

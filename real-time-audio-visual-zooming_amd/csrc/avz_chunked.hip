@@ -115,6 +115,34 @@ __device__ __forceinline__ float inv_wsum(int m) {
   return 1.0f / (wa * wa + wb * wb);
 }
 
+// Lane constants of the chain kernels (FFT twiddle registers, lane map, window terms,
+// the synthesis OLA normalisation and inverse window terms): computed once per block by
+// the persistent kernels, not per item (the fp64 sincospi calls cost 1-2 us per item).
+template <int N>
+struct LaneConst {
+  typename KCfg<N>::Fft fft;
+  LaneMap<N> lm;
+  WinCoef<N> wc;
+  float inv[4];      // synthesis OLA: 1 / window-square sum of samples m0 .. m0 + 3
+  float wi_c, wi_s;  // synthesis, N = 1024: 0.25 cos / sin(2 pi n0 / N), x1 inverse layout
+  __device__ __forceinline__ void init(int tid) {
+    const int lane = tid & 63;
+    fft.init(lane);
+    lm.init(lane);
+    wc.init(lm);
+    const int m0 = 4 * (tid % (N / 8));  // synthesis OLA role (N/2 / 4 float4 groups)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(m0 + i);
+    wi_c = wi_s = 0.0f;
+    if constexpr (N == 1024) {
+      double sn, cs;
+      sincospi(2.0 * ((lane & 31) + 512 * (lane >> 5)) / N, &sn, &cs);
+      wi_c = (float)(0.25 * cs);
+      wi_s = (float)(0.25 * sn);
+    }
+  }
+};
+
 // Analysis window of a lane's points: register r holds sample n0 + IN_STRIDE r, weight
 // w = a0 - ac cos(2 pi IN_STRIDE r / N) + as sin(...) (angle addition on the lane's n0).
 // Registers PPL/2 apart are N/2 samples apart, where the periodic Hann window satisfies
@@ -281,7 +309,7 @@ __device__ __forceinline__ float irm_gain(cf zr, cf zrp) {
 struct NoTw {};
 template <int N, int MASK, bool IRM, class TW>
 __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char* lds, int c,
-                                              int b, const TW& tw_reg) {
+                                              int b, const TW& tw_reg, const LaneConst<N>& K) {
   using C = KCfg<N>;
   using G = CGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
@@ -315,12 +343,9 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   const int nframes = min(kChunk, T - t0);
   const int nstep = (nframes + FB - 1) / FB;
 
-  typename C::Fft fft;
-  fft.init(lane);
-  LaneMap<N> lm;
-  lm.init(lane);
-  WinCoef<N> wc;
-  wc.init(lm);
+  const typename C::Fft fft = K.fft;
+  const LaneMap<N> lm = K.lm;
+  WinCoef<N> wc = K.wc;
   if (SHARE && lm.grp) {  // rotated frame: window halves swapped
     wc.ac = -wc.ac;
     wc.as = -wc.as;
@@ -678,11 +703,15 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysi
     if (AVZ_SHARE_LOADS && MASK != MASK_IPD && (threadIdx.x & 32)) {  // rotated frames: (-1)^k1 (pair_loads)
       static_for<0, 16>([&](auto i) { tw_reg[2 * i] = cf{-tw_reg[2 * i].x, -tw_reg[2 * i].y}; });
     }
+    LaneConst<N> K;
+    K.init(threadIdx.x);
     for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-      analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, tw_reg);
+      analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, tw_reg, K);
   } else {
+    LaneConst<N> K;
+    K.init(threadIdx.x);
     for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-      analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, NoTw{});
+      analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, NoTw{}, K);
   }
 }
 
@@ -821,7 +850,7 @@ __device__ void fused_finalize(const ChainArgs& A, int b, int T, int nch, float*
 
 template <int N, int PF, bool SPEC, bool FUSED>
 __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char* lds, int c,
-                                               int b) {
+                                               int b, const LaneConst<N>& K) {
   static_assert(!SPEC || PF == PF_NONE, "spectrum input carries its own post-filter");
   using C = KCfg<N>;
   using G = CGeo<N>;
@@ -859,12 +888,9 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   const rsrc_t r_heads = make_rsrc(A.heads + (long long)b * A.nchunk * H, (long long)A.nchunk * H);
   const rsrc_t r_tails = make_rsrc(A.tails + (long long)b * A.nchunk * H, (long long)A.nchunk * H);
 
-  typename C::Fft fft;
-  fft.init(lane);
-  LaneMap<N> lm;
-  lm.init(lane);
-  WinCoef<N> wc;
-  wc.init(lm);
+  const typename C::Fft fft = K.fft;
+  const LaneMap<N> lm = K.lm;
+  const WinCoef<N> wc = K.wc;
   const int my_slot = wave * C::FPW + lm.grp;
   cf* my_spec = slot_ptr<N>(lds, my_slot);
 
@@ -952,7 +978,8 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   const int sgrp = tid / M4;
   float inv[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(m0 + i);
+  for (int i = 0; i < 4; ++i) inv[i] = K.inv[i];
+  static_assert(M4 == N / 8, "LaneConst's OLA role");
   float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);  // previous frame's second half (sgrp 0)
   float* outb = A.out + (long long)b * A.out_stride;
   float peak = 0.0f;
@@ -969,10 +996,8 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       wh_s[e] = (float)(0.25 * sn);
     }
   } else if constexpr (N == 1024) {
-    double sn, cs;
-    sincospi(2.0 * ((lane & 31) + 512 * (lane >> 5)) / N, &sn, &cs);
-    wi_c = (float)(0.25 * cs);
-    wi_s = (float)(0.25 * sn);
+    wi_c = K.wi_c;
+    wi_s = K.wi_s;
   }
 
   lds_barrier();  // twiddle table
@@ -1359,8 +1384,10 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_syn
   KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
   const int n_items = gx * A.batch;
+  LaneConst<N> K;
+  K.init(threadIdx.x);
   for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-    synthesis_item<N, PF, SPEC, FUSED>(A, lds, it % gx, it / gx);
+    synthesis_item<N, PF, SPEC, FUSED>(A, lds, it % gx, it / gx, K);
 }
 
 // Finalize of utterance b inside the synthesis kernel, run by the block whose item was the

@@ -121,7 +121,10 @@ struct KCfg<512> {
 #ifdef AVZ_B512
   static constexpr int BLOCKS_PER_CU = AVZ_B512;
 #else
-  static constexpr int BLOCKS_PER_CU = 2;
+  // analysis at 3 blocks (12 waves) per CU: 168 VGPRs, 3 x 35 KB LDS; 97.9 -> 81.0 us at
+  // B = 256 (profiles/r03/n512_occupancy.txt); 4 spills and runs 85 us, the synthesis
+  // gains nothing from 3 (spills at 168 VGPRs)
+  static constexpr int BLOCKS_PER_CU = 3;
 #endif
 #ifdef AVZ_SB512
   static constexpr int SYN_BLOCKS_PER_CU = AVZ_SB512;

@@ -478,8 +478,8 @@ struct Fft512x2 {
   static constexpr int N = 512;
   static constexpr int PPL = 16;
   static constexpr int SCRATCH_F2 = 16 * 34;  // per group
-  cf P[4], Q[4];  // W512^{j i}, W512^{4 j i}
-  float sgn;      // step-2 half: (lane >> 4) & 1
+  cf tw[15];  // W512^{j k}, k = 1 .. 15 (as P[k & 3] Q[k >> 2], P = W512^{j i}, Q = W512^{4 j i})
+  float sgn;  // step-2 half: (lane >> 4) & 1
   int j, k1, h2;
 
   __device__ __forceinline__ void init(int lane) {
@@ -487,10 +487,15 @@ struct Fft512x2 {
     k1 = lane & 15;
     h2 = (lane >> 4) & 1;
     sgn = h2 ? -1.0f : 1.0f;
+    cf P[4], Q[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) P[i] = unit_root((double)(j * i) / N);
 #pragma unroll
     for (int i = 0; i < 4; ++i) Q[i] = unit_root((double)(4 * j * i) / N);
+    // the products the transform used to form per call, formed once (same rounding)
+    static_for<1, 16>([&](auto k) {
+      tw[k - 1] = ((k & 3) == 0) ? Q[k >> 2] : c_mul(P[k & 3], Q[k >> 2]);
+    });
   }
 
   __device__ static void fill_twiddles(cf*, int, int) {}
@@ -498,10 +503,7 @@ struct Fft512x2 {
   // v: x_g[j + 32 r] in; X_g[k1 + 16 r + 256 h] out. scratch: this lane group's slot.
   __device__ __forceinline__ void forward(cf (&v)[16], cf* scratch, const cf* = nullptr) const {
     dft16(v);  // reg k holds A[j][k]
-    static_for<1, 16>([&](auto k) {
-      const cf tw = ((k & 3) == 0) ? Q[k >> 2] : c_mul(P[k & 3], Q[k >> 2]);
-      v[k] = c_mul(v[k], tw);
-    });
+    static_for<1, 16>([&](auto k) { v[k] = c_mul(v[k], tw[k - 1]); });
     static_for<0, 16>([&](auto k) { scratch[k * 34 + j] = v[k]; });
     __builtin_amdgcn_wave_barrier();
     static_for<0, 16>([&](auto r) { v[r] = scratch[k1 * 34 + 2 * r + h2]; });
