@@ -45,6 +45,13 @@ namespace avz {
 #ifndef AVZ_SYN_HALF
 #define AVZ_SYN_HALF 0
 #endif
+#ifndef AVZ_SYN_PREWIN
+#define AVZ_SYN_PREWIN 0
+#endif
+// Round-chained synthesis (launch_synth_rounds): off, measured slower
+#ifndef AVZ_SYN_ROUNDS
+#define AVZ_SYN_ROUNDS 0
+#endif
 // The chain's finalize folded into the synthesis kernel: the last chunk item of an
 // utterance to finish (arrival ticket) writes its seams and peak and, for peak
 // normalisation, rescales the utterance in place (fused_finalize).
@@ -89,6 +96,26 @@ struct CGeo {
   static_assert(BLOCKS * LDS_BYTES <= 160 * 1024, "resident blocks per CU");
 };
 
+// Synthesis geometry: as CGeo with SYN_R frames per lane group per step (NSLOT frame slots,
+// each a lane group's transform area; slot s is "virtual wave" s / FPW of the slot area).
+template <int N>
+struct SGeo {
+  using C = KCfg<N>;
+  static constexpr int NT = kCThreads;
+  static constexpr int NWAVE = NT / 64;
+  static constexpr int R = C::SYN_R;
+  static constexpr int H = N / 2;
+  static constexpr int F = N / 2 + 1;
+  static constexpr int NSLOT = NWAVE * C::FPW * R;
+  static constexpr int BPT = (N / 2) / NT;
+  static constexpr int SLOT_LDS = NWAVE * C::WAVE_BYTES * R;
+  static constexpr int TW_OFF = SLOT_LDS;
+  static constexpr int MISC_OFF = TW_OFF + C::TW_BYTES;
+  static constexpr int LDS_BYTES = MISC_OFF + 64;
+  static constexpr int BLOCKS = C::SYN_BLOCKS_PER_CU;
+  static_assert(BLOCKS * LDS_BYTES <= 160 * 1024, "resident synthesis blocks per CU");
+};
+
 // Per-lane analysis window * 1/sum(win) and synthesis window * sum(win)/N terms.
 template <int N>
 struct WinCoef {
@@ -125,6 +152,9 @@ struct LaneConst {
   WinCoef<N> wc;
   float inv[4];      // synthesis OLA: 1 / window-square sum of samples m0 .. m0 + 3
   float wi_c, wi_s;  // synthesis, N = 1024: 0.25 cos / sin(2 pi n0 / N), x1 inverse layout
+  // synthesis forward window weights of registers r < PPL/2 (window_apply's w; the upper
+  // half takes 2 a0 - w), formed once instead of per frame
+  float ww[KCfg<N>::PPL / 2];
   __device__ __forceinline__ void init(int tid) {
     const int lane = tid & 63;
     fft.init(lane);
@@ -133,6 +163,14 @@ struct LaneConst {
     const int m0 = 4 * (tid % (N / 8));  // synthesis OLA role (N/2 / 4 float4 groups)
 #pragma unroll
     for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(m0 + i);
+    {
+      using C = KCfg<N>;
+      static_for<0, C::PPL / 2>([&](auto r) {
+        constexpr int j = (C::IN_STRIDE * 32 / N) * r;
+        constexpr float cr = W32::c[j % 32], sr = -W32::s[j % 32];
+        ww[r] = fmaf(wc.as, sr, fmaf(-wc.ac, cr, wc.a0));
+      });
+    }
     wi_c = wi_s = 0.0f;
     if constexpr (N == 1024) {
       double sn, cs;
@@ -195,6 +233,22 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
     w |= (ibm_noise(v[k], zp) ? 1u : 0u) << k;
   });
   reinterpret_cast<uint32_t*>(spec)[l] = w;
+}
+
+// window_fft with the lane's window weights precomputed (LaneConst::ww): the synthesis
+// kernel has the registers for them, the analysis kernel does not.
+template <int N>
+__device__ __forceinline__ void window_fft_pre(cf (&v)[KCfg<N>::PPL], const float (&ww)[KCfg<N>::PPL / 2],
+                                               float a0, const typename KCfg<N>::Fft& fft, cf* spec,
+                                               const cf* twid, const LaneMap<N>& lm) {
+  using C = KCfg<N>;
+  const float a2 = a0 + a0;
+  static_for<0, C::PPL / 2>([&](auto r) {
+    v[r] = c_scale(v[r], ww[r]);
+    v[r + C::PPL / 2] = c_scale(v[r + C::PPL / 2], a2 - ww[r]);
+  });
+  fft.forward(v, spec, twid);
+  static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
 }
 
 template <int N>
@@ -847,13 +901,15 @@ __global__ void __launch_bounds__(kSrpThreads) avz_srp_kernel(ChainArgs A, SrpAr
 // S[b][k][t]) instead of the forward FFT of the mixture and the apply step.
 template <int N>
 __device__ void fused_finalize(const ChainArgs& A, int b, int T, int nch, float* red);
+template <int N>
+__device__ __forceinline__ void finalize_item(const ChainArgs& A, int c, int b, float* red);
 
 template <int N, int PF, bool SPEC, bool FUSED>
 __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char* lds, int c,
                                                int b, const LaneConst<N>& K) {
   static_assert(!SPEC || PF == PF_NONE, "spectrum input carries its own post-filter");
   using C = KCfg<N>;
-  using G = CGeo<N>;
+  using G = SGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
   constexpr int FB = NSLOT;           // frames per step
   constexpr int NPAIR = FB / 2;       // packed inverse FFTs per step
@@ -893,22 +949,34 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   const WinCoef<N> wc = K.wc;
   const int my_slot = wave * C::FPW + lm.grp;
   cf* my_spec = slot_ptr<N>(lds, my_slot);
+  // SGeo::R > 1: the lane group also transforms frames my_slot + NWAVE FPW q, q < R
+  constexpr int RSTRIDE = G::NWAVE * C::FPW;
 
   const float* mixb = A.mix + (long long)b * A.mix_stride;
   const rsrc_t r_m0 = make_rsrc(mixb, L), r_m1 = make_rsrc(mixb + A.ch_stride, L);
   cf v[PPL];
-  auto issue_loads = [&](int step) {
-    const int s0 = (t0 + step * FB + my_slot) * H - N / 2 + lm.in0;
-    if (t0 + step * FB + wave * C::FPW >= 1) {  // wave-uniform: no negative sample index
+  cf vq[G::R > 1 ? G::R - 1 : 1][G::R > 1 ? PPL : 1];  // frames q >= 1 of the step
+  auto load_frame = [&](cf (&x)[PPL], int frame, int wave_frame) {
+    const int s0 = frame * H - N / 2 + lm.in0;
+    if (wave_frame >= 1) {  // wave-uniform: no negative sample index
       static_for<0, PPL>([&](auto r) {
-        v[r].x = bload_nn(r_m0, s0 + C::IN_STRIDE * r);
-        v[r].y = bload_nn(r_m1, s0 + C::IN_STRIDE * r);
+        x[r].x = bload_nn(r_m0, s0 + C::IN_STRIDE * r);
+        x[r].y = bload_nn(r_m1, s0 + C::IN_STRIDE * r);
       });
     } else {
       static_for<0, PPL>([&](auto r) {
-        v[r].x = bload(r_m0, s0 + C::IN_STRIDE * r);
-        v[r].y = bload(r_m1, s0 + C::IN_STRIDE * r);
+        x[r].x = bload(r_m0, s0 + C::IN_STRIDE * r);
+        x[r].y = bload(r_m1, s0 + C::IN_STRIDE * r);
       });
+    }
+  };
+  auto issue_loads = [&](int step) {
+    const int fb = t0 + step * FB;
+    load_frame(v, fb + my_slot, fb + wave * C::FPW);
+    if constexpr (G::R > 1) {
+#pragma unroll
+      for (int q = 1; q < G::R; ++q)
+        load_frame(vq[q - 1], fb + my_slot + q * RSTRIDE, fb + wave * C::FPW + q * RSTRIDE);
     }
   };
   AVZ_STAMP_DECL();
@@ -1010,7 +1078,22 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     AVZ_STAMP(5);
 #endif
     if constexpr (!SPEC) {
+#if AVZ_SYN_PREWIN
+      window_fft_pre<N>(v, K.ww, wc.a0, fft, my_spec, twid, lm);
+      if constexpr (G::R > 1) {
+#pragma unroll
+        for (int q = 1; q < G::R; ++q)
+          window_fft_pre<N>(vq[q - 1], K.ww, wc.a0, fft, slot_ptr<N>(lds, my_slot + q * RSTRIDE),
+                            twid, lm);
+      }
+#else
       window_fft<N>(v, wc, fft, my_spec, twid, lm);
+      if constexpr (G::R > 1) {
+#pragma unroll
+        for (int q = 1; q < G::R; ++q)
+          window_fft<N>(vq[q - 1], wc, fft, slot_ptr<N>(lds, my_slot + q * RSTRIDE), twid, lm);
+      }
+#endif
       // x2 with the x1 inverse: the next step's loads fly through apply, inverse FFT and
       // OLA. x1 and the two-wave x2 inverse issue them after the inverse FFT, whose
       // registers they are (measured: issuing them here on the two pairless waves, or
@@ -1379,15 +1462,37 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
 // Persistent grid over (chunk, utterance) items, as avz_analysis_kernel.
 template <int N, int PF, bool SPEC = false, bool FUSED = false>
 __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_synthesis_kernel(ChainArgs A) {
-  using G = CGeo<N>;
+  using G = SGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
   KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
-  const int n_items = gx * A.batch;
   LaneConst<N> K;
   K.init(threadIdx.x);
-  for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-    synthesis_item<N, PF, SPEC, FUSED>(A, lds, it % gx, it / gx, K);
+  // finalize items of the previous launch's utterances, run by the upper half of the grid
+  // before its synthesis items and by the lower half after them, so the resident blocks of
+  // a CU (dispatched a grid half apart) mostly pair an HBM-bound finalize item with a
+  // compute-bound synthesis item
+  const int nsyn = gx * A.syn_nb;
+  if constexpr (AVZ_SYN_ROUNDS) {  // compiled out otherwise: the finalize item costs registers
+    float* red = reinterpret_cast<float*>(lds + G::MISC_OFF);
+    const int nfin = gx * A.fin_nb;
+    auto fin_items = [&]() {
+      for (int it = blockIdx.x; it < nfin; it += gridDim.x) {
+        __syncthreads();  // red[] of the previous item
+        finalize_item<N>(A, it % gx, A.fin_b0 + it / gx, red);
+      }
+    };
+    const bool fin_first = blockIdx.x >= gridDim.x / 2;
+    if (fin_first) fin_items();
+    for (int it = blockIdx.x; it < nsyn; it += gridDim.x) {
+      if (nfin > 0) __syncthreads();
+      synthesis_item<N, PF, SPEC, FUSED>(A, lds, it % gx, A.syn_b0 + it / gx, K);
+    }
+    if (!fin_first) fin_items();
+  } else {
+    for (int it = blockIdx.x; it < nsyn; it += gridDim.x)
+      synthesis_item<N, PF, SPEC, FUSED>(A, lds, it % gx, A.syn_b0 + it / gx, K);
+  }
 }
 
 // Finalize of utterance b inside the synthesis kernel, run by the block whose item was the
@@ -1455,11 +1560,11 @@ __device__ void fused_finalize(const ChainArgs& A, int b, int T, int nch, float*
 }
 
 // ================================ finalize ================================
+// One (chunk, utterance) item: the standalone finalize kernel's block, or a finalize item
+// run inside the next synthesis launch (red: NWAVE floats of LDS).
 template <int N>
-__global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
+__device__ __forceinline__ void finalize_item(const ChainArgs& A, int c, int b, float* red) {
   constexpr int NT = kCThreads, H = N / 2, NWAVE = NT / 64;
-  __shared__ float red[NWAVE];
-  const int c = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int L = utt_len(A, b);
   if (L < N) {
@@ -1542,6 +1647,12 @@ __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
   }
 }
 
+template <int N>
+__global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
+  __shared__ float red[kCThreads / 64];
+  finalize_item<N>(A, blockIdx.x, A.fin_b0 + blockIdx.y, red);
+}
+
 }  // namespace avz
 
 using namespace avz;
@@ -1551,15 +1662,48 @@ extern "C" int avz_chunk_frames(void) { return kChunk; }
 static int resident_cus();
 
 // The synthesis launch of the chain and of the stage exports (persistent grid).
+// One synthesis launch over utterances [a->syn_b0, + syn_nb) with the finalize items of
+// [fin_b0, + fin_nb) in the same persistent grid.
 template <int N, int PF, bool FUSED = false>
 static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
-  constexpr int lds = CGeo<N>::LDS_BYTES;
+  constexpr int lds = SGeo<N>::LDS_BYTES;
   if (!lds_ready<avz_synthesis_kernel<N, PF, false, FUSED>>(lds)) return -3;
-  const int n_items = nch * a->batch;
+  const int n_items = nch * std::max(a->syn_nb, a->fin_nb);
+  if (n_items == 0) return 0;
   const dim3 sgrid((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus()));
   hipExtLaunchKernelGGL((avz_synthesis_kernel<N, PF, false, FUSED>), sgrid, dim3(kCThreads), lds,
                         st, e0, e1, 0, *a);
+  return 0;
+}
+
+// The chain's synthesis + finalize (non-fused): the batch is synthesised in rounds of as
+// many utterances as the resident grid holds; every round's launch also runs the previous
+// round's finalize items, so that HBM-bound pass overlaps compute-bound synthesis, and only
+// the last round's finalize runs as its own kernel. One round (or AVZ_SYN_ROUNDS 0): one
+// synthesis launch and one finalize launch.
+template <int N, int PF>
+static int launch_synth_rounds(const ChainArgs* a, hipStream_t st, hipEvent_t e4, hipEvent_t e5,
+                               hipEvent_t e6, hipEvent_t e7) {
+  const int nch = (a->max_frames + kChunk - 1) / kChunk;
+  const int slots = KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus();
+  const int per_round = AVZ_SYN_ROUNDS ? std::max(1, slots / nch) : a->batch;
+  ChainArgs s = *a;
+  int prev_b0 = 0, prev_nb = 0;
+  for (int b0 = 0; b0 < a->batch; b0 += per_round) {
+    s.syn_b0 = b0;
+    s.syn_nb = std::min(per_round, a->batch - b0);
+    s.fin_b0 = prev_b0;
+    s.fin_nb = prev_nb;
+    const bool first = b0 == 0, last = b0 + per_round >= a->batch;
+    if (launch_synthesis<N, PF>(&s, st, first ? e4 : nullptr, last ? e5 : nullptr) != 0) return -3;
+    prev_b0 = s.syn_b0;
+    prev_nb = s.syn_nb;
+  }
+  ChainArgs f = *a;
+  f.fin_b0 = prev_b0;
+  hipExtLaunchKernelGGL(avz_finalize_kernel<N>, dim3(nch, prev_nb), dim3(kCThreads), 0, st, e6,
+                        e7, 0, f);
   return 0;
 }
 
@@ -1614,13 +1758,18 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
 #if AVZ_FUSED_FIN
   (void)k3;
   (void)grid;
-  if (launch_synthesis<N, PF, true>(a, st, evt(4), evt(5)) != 0) return -3;
+  ChainArgs af = *a;
+  af.syn_b0 = 0;
+  af.syn_nb = a->batch;
+  af.fin_nb = 0;
+  if (launch_synthesis<N, PF, true>(&af, st, evt(4), evt(5)) != 0) return -3;
   if (evt(6) && (hipEventRecord(evt(6), st) != hipSuccess ||  // finalize: fused (0 ms)
                  hipEventRecord(evt(7), st) != hipSuccess))
     return -3;
 #else
-  if (launch_synthesis<N, PF>(a, st, evt(4), evt(5)) != 0) return -3;
-  hipExtLaunchKernelGGL(k3, grid, dim3(kCThreads), 0, st, evt(6), evt(7), 0, *a);
+  (void)k3;
+  (void)grid;
+  if (launch_synth_rounds<N, PF>(a, st, evt(4), evt(5), evt(6), evt(7)) != 0) return -3;
 #endif
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
@@ -1729,7 +1878,7 @@ extern "C" int avz_launch_covariance(int n_fft, int mask_mode, const ChainArgs* 
 
 template <int N, int PF, bool SPEC>
 static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
-  constexpr int lds = CGeo<N>::LDS_BYTES;
+  constexpr int lds = SGeo<N>::LDS_BYTES;
   if (SPEC && !lds_ready<avz_synthesis_kernel<N, PF, SPEC>>(lds)) return -3;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
@@ -1739,14 +1888,19 @@ static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
   if (a->peak && a->normalize != NORM_PEAK &&
       hipMemsetAsync(a->peak, 0, sizeof(float) * a->batch, st) != hipSuccess)
     return -3;
+  ChainArgs s = *a;  // one synthesis launch over the batch, then the finalize kernel
+  s.syn_b0 = 0;
+  s.syn_nb = a->batch;
+  s.fin_b0 = 0;
+  s.fin_nb = 0;
   if constexpr (SPEC) {
     hipLaunchKernelGGL((avz_synthesis_kernel<N, PF, SPEC>),
                        dim3((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus())),
-                       dim3(kCThreads), lds, st, *a);
+                       dim3(kCThreads), lds, st, s);
   } else {
-    if (launch_synthesis<N, PF>(a, st, nullptr, nullptr) != 0) return -3;
+    if (launch_synthesis<N, PF>(&s, st, nullptr, nullptr) != 0) return -3;
   }
-  hipLaunchKernelGGL(avz_finalize_kernel<N>, dim3(nch, a->batch), dim3(kCThreads), 0, st, *a);
+  hipLaunchKernelGGL(avz_finalize_kernel<N>, dim3(nch, a->batch), dim3(kCThreads), 0, st, s);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -106,6 +106,7 @@ struct KCfg<1024> {
   static constexpr int TW_BYTES = 32 * 32 * 8;  // block-shared W1024^{l k1} table
   static constexpr int BLOCKS_PER_CU = 2;
   static constexpr int SYN_BLOCKS_PER_CU = 2;
+  static constexpr int SYN_R = 1;  // synthesis frames per lane group per step
 };
 #endif
 template <>
@@ -130,6 +131,13 @@ struct KCfg<512> {
   static constexpr int SYN_BLOCKS_PER_CU = AVZ_SB512;
 #else
   static constexpr int SYN_BLOCKS_PER_CU = 2;
+#endif
+  // synthesis frames per lane group per step: 2 -> 16 frames (and 8 packed inverse pairs,
+  // two per wave) per step in the same 70 KB of LDS as N = 1024's 8
+#ifdef AVZ_SYN_R512
+  static constexpr int SYN_R = AVZ_SYN_R512;
+#else
+  static constexpr int SYN_R = 2;
 #endif
 };
 

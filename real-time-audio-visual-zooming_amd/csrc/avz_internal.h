@@ -54,6 +54,10 @@ struct ChainArgs {
   long long spec_sb, spec_sf; // complex elements; t stride 1
   int spec_frames;            // frames present in S (frames >= spec_frames read as zero)
   int cov_only;               // solve kernel: write cov_out only (the covariance stage export)
+  // synthesis launch: utterances [syn_b0, syn_b0 + syn_nb) are synthesised and the
+  // finalize items of utterances [fin_b0, fin_b0 + fin_nb) (synthesised by the previous
+  // launch) run in the same grid; the standalone finalize kernel starts at fin_b0
+  int syn_b0, syn_nb, fin_b0, fin_nb;
   int* flag;                  // [B] item-level (batch_mvdr) fallback flags, zeroed per call
   void* const* events;        // host-only: (start, stop) hipEvent_t pairs of the 4 launches, or null
   int n_events;               // host-only: how many of them to use (8, or 2: analysis only)

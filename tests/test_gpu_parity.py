@@ -296,3 +296,39 @@ def test_ipd_identical_channels(avz, gpu_device):
         assert np.min(dphi[k][dphi[k] > 0], initial=0.0) < 1e-6, (k, np.min(dphi[k]))
     print(f"one differing sample: mask decisions differing from the reference: "
           f"{len(dev_bins)} bins, all angle ties (|d angle| < 1e-6 rad)")
+
+
+def test_multi_round_ragged_batch_equals_single_runs(avz, gpu_device):
+    """A batch larger than one resident synthesis round (128 utterances of 4 chunks at
+    N = 1024 on 256 CUs) with ragged lengths: the round-chained synthesis runs every
+    round's finalize items inside the next round's launch. Every utterance must equal its
+    own single-utterance run bitwise (same kernels, same per-utterance arithmetic) and the
+    peak-normalised output must peak at peak / (peak + eps)."""
+    from avz import synth
+    B, S = 300, 64000
+    dm, dt, di = synth.make_batch_device(B, start=77, n_samples=S, n_interferers=2,
+                                         device=gpu_device, rng="philox")
+    rng = np.random.default_rng(5)
+    lens = rng.integers(2000, S + 1, size=B).astype(np.int32)
+    lens[:3] = [S, 1024, 16001]
+    plan = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
+                        normalize="peak", max_batch=B, max_samples=S)
+    lt = torch.from_numpy(lens).to(gpu_device)
+    out, peak = plan.run(dm, lt, max_len=S, ref_tgt=dt, ref_int=di)
+    out, peak = out.clone(), peak.clone()
+    one = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
+                       normalize="peak", max_batch=1, max_samples=S)
+    for b in (0, 1, 2, 127, 128, 129, 200, 255, 256, 299):
+        L = int(lens[b])
+        o1, p1 = one.run(dm[b:b + 1, :, :L].contiguous(), ref_tgt=dt[b:b + 1, :L].contiguous(),
+                         ref_int=di[b:b + 1, :L].contiguous())
+        n = one.out_len(L)
+        # bitwise, NaN included: an utterance whose whole output is 0 normalises to 0/0
+        # as the reference's s_out / max|s_out| does (norm_eps 0)
+        torch.testing.assert_close(out[b, :n], o1[0, :n], rtol=0, atol=0, equal_nan=True)
+        torch.testing.assert_close(peak[b], p1[0], rtol=0, atol=0, equal_nan=True)
+    n_out = [plan.out_len(int(L)) for L in lens]
+    amax = torch.stack([out[b, :n_out[b]].abs().max() for b in range(B)]).double()
+    ok = peak > 0  # short utterances inside a silent stretch of the scene beamform to 0
+    assert int(ok.sum()) >= 0.95 * B
+    assert torch.allclose(amax[ok], torch.ones_like(amax[ok]), rtol=1e-6, atol=0)
