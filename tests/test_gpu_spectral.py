@@ -187,3 +187,21 @@ def test_apply_istft_gain_equals_ibm_postfilter(gpu_device):
     out_s, _ = plan.apply_istft(m, w_f, gain=gain.contiguous())
     n = plan.out_len(32000)
     assert torch.max(torch.abs(out_s[:, :n] - out_f[:, :n])).item() <= 2e-4
+
+
+@pytest.mark.parametrize("T", [37, 64, 100])
+def test_batch_mvdr_frame_counts_vs_oracle(gpu_device, T):
+    """Both spectral layouts: <= 64 frames (16 lanes per row, frames in registers) and
+    longer spectra (one wave per row); random complex64 Y and a uniform mask, against the
+    oracle's batch_mvdr (tf_lite_version/inference.py:85-179 restated)."""
+    from avz import spectral
+    rng = np.random.default_rng(T)
+    F = 513
+    Y = (rng.standard_normal((2, F, T)) + 1j * rng.standard_normal((2, F, T))).astype(np.complex64)
+    M = rng.random((F, T)).astype(np.float32)
+    f_bins = np.fft.rfftfreq(1024, 1 / 16000)
+    d = spectral.get_all_steering_vectors(f_bins, 90.0, 0.04, 343.0)
+    ref = O.batch_mvdr(Y, M, f_bins, d, 1e-5)
+    S = spectral.batch_mvdr(Y, M, f_bins, d, 1e-5)
+    err = np.abs(S - ref).max() / np.abs(ref).max()
+    assert err <= 1e-5, err

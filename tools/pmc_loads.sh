@@ -6,6 +6,7 @@
 #   gpurun -- 'bash tools/pmc_loads.sh <tag>'
 set -o pipefail
 tag=${1:-loads}
+shift || true
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
