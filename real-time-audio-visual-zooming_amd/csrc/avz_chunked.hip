@@ -1475,11 +1475,13 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_syn
   const int nsyn = gx * A.syn_nb;
   if constexpr (AVZ_SYN_ROUNDS) {  // compiled out otherwise: the finalize item costs registers
     float* red = reinterpret_cast<float*>(lds + G::MISC_OFF);
-    const int nfin = gx * A.fin_nb;
+    constexpr int FCH = N >= 1024 ? 1 : 1024 / N;  // kFinChunks<N> (defined with finalize)
+    const int fg = (gx + FCH - 1) / FCH;
+    const int nfin = fg * A.fin_nb;
     auto fin_items = [&]() {
       for (int it = blockIdx.x; it < nfin; it += gridDim.x) {
         __syncthreads();  // red[] of the previous item
-        finalize_item<N>(A, it % gx, A.fin_b0 + it / gx, red);
+        finalize_item<N>(A, it % fg, A.fin_b0 + it / fg, red);
       }
     };
     const bool fin_first = blockIdx.x >= gridDim.x / 2;
@@ -1560,20 +1562,28 @@ __device__ void fused_finalize(const ChainArgs& A, int b, int T, int nch, float*
 }
 
 // ================================ finalize ================================
-// One (chunk, utterance) item: the standalone finalize kernel's block, or a finalize item
-// run inside the next synthesis launch (red: NWAVE floats of LDS).
+// Finalize blocks handle FCH consecutive chunks (N = 512: two, so a block rescales the same
+// 64 KB as N = 1024's one chunk instead of twice as many blocks moving 31 KB each).
 template <int N>
-__device__ __forceinline__ void finalize_item(const ChainArgs& A, int c, int b, float* red) {
-  constexpr int NT = kCThreads, H = N / 2, NWAVE = NT / 64;
+constexpr int kFinChunks = N >= 1024 ? 1 : 1024 / N;
+
+// One finalize item: chunks FCH q .. FCH q + FCH - 1 of utterance b — the standalone
+// finalize kernel's block, or a finalize item run inside the next synthesis launch (red:
+// NWAVE floats of LDS).
+template <int N>
+__device__ __forceinline__ void finalize_item(const ChainArgs& A, int q, int b, float* red) {
+  constexpr int NT = kCThreads, H = N / 2, NWAVE = NT / 64, FCH = kFinChunks<N>;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int c0 = FCH * q;
   const int L = utt_len(A, b);
   if (L < N) {
-    if (c == 0 && tid == 0 && A.peak) A.peak[b] = __builtin_nanf("");
+    if (c0 == 0 && tid == 0 && A.peak) A.peak[b] = __builtin_nanf("");
     return;
   }
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
-  if (c >= nch) return;
+  if (c0 >= nch) return;
+  const int cend = min(c0 + FCH, nch);  // chunks c0 .. cend - 1
   const float* heads = A.heads + (long long)b * A.nchunk * H;
   const float* tails = A.tails + (long long)b * A.nchunk * H;
   // boundary segment 32 cc - 1 = tail(cc - 1) + head(cc), cc = 1 .. nch - 1
@@ -1582,12 +1592,12 @@ __device__ __forceinline__ void finalize_item(const ChainArgs& A, int c, int b, 
   };
   float* outb = A.out + (long long)b * A.out_stride;
   if (A.normalize != NORM_PEAK) {
-    // un-normalised output (the batch driver's deferred normalisation): each chunk writes
-    // its own seam and folds its max (chunk 0: the interiors' max) into peak[b], zeroed by
-    // the analysis kernel, with an atomicMax on the float's bits (non-negative floats
-    // order as unsigned ints) — no redundant reads of the other seams
+    // un-normalised output (the batch driver's deferred normalisation): each block writes
+    // its chunks' seams and folds their max (chunk 0: the interiors' max) into peak[b],
+    // zeroed by the analysis kernel, with an atomicMax on the float's bits (non-negative
+    // floats order as unsigned ints) — no redundant reads of the other seams
     float pm = 0.0f;
-    if (c >= 1) {
+    for (int c = max(c0, 1); c < cend; ++c) {
       const long long j = (long long)kChunk * c - 1;
       for (int m = tid; m < H; m += NT) {
         const float x = boundary(c, m);
@@ -1599,26 +1609,30 @@ __device__ __forceinline__ void finalize_item(const ChainArgs& A, int c, int b, 
     if (lane == 0) red[wave] = pm;
     __syncthreads();
     if (tid == 0 && A.peak) {
-      float q = (c == 0) ? __uint_as_float(A.peak_u[b]) : 0.0f;
+      float qm = (c0 == 0) ? __uint_as_float(A.peak_u[b]) : 0.0f;
 #pragma unroll
-      for (int w = 0; w < NWAVE; ++w) q = fmaxf(q, red[w]);
-      atomicMax(reinterpret_cast<unsigned int*>(A.peak + b), __float_as_uint(q));
+      for (int w = 0; w < NWAVE; ++w) qm = fmaxf(qm, red[w]);
+      atomicMax(reinterpret_cast<unsigned int*>(A.peak + b), __float_as_uint(qm));
     }
     return;
   }
-  // The chunk's interior segments 32c .. 32c+30 are read into registers first: their loads
+  // The chunks' interior segments 32c .. 32c+30 are read into registers first: their loads
   // do not depend on the utterance peak, so they stream while the seam maxima below are
   // fetched (all blocks are resident at once; reading them after the peak left every
   // block waiting on its seam loads before any bulk traffic started).
   constexpr int U = ((kChunk - 1) * H / 4 + NT - 1) / NT;
-  const int j0 = kChunk * c, j1 = min(kChunk * c + kChunk - 1, T - 1);
-  float4* o4 = reinterpret_cast<float4*>(outb + (long long)j0 * H);
-  const int n4 = (j1 - j0) * H / 4;
-  float4 xin[U];
+  float4 xin[FCH][U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = tid + u * NT;
-    if (i < n4) xin[u] = o4[i];
+  for (int g = 0; g < FCH; ++g) {
+    const int c = c0 + g;
+    const int j0 = kChunk * c, j1 = min(kChunk * c + kChunk - 1, T - 1);
+    const float4* o4 = reinterpret_cast<const float4*>(outb + (long long)j0 * H);
+    const int n4 = c < cend ? (j1 - j0) * H / 4 : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * NT;
+      if (i < n4) xin[g][u] = o4[i];
+    }
   }
   float pk = 0.0f;
 #pragma unroll 4
@@ -1630,19 +1644,26 @@ __device__ __forceinline__ void finalize_item(const ChainArgs& A, int c, int b, 
   pk = __uint_as_float(A.peak_u[b]);
 #pragma unroll
   for (int w = 0; w < NWAVE; ++w) pk = fmaxf(pk, red[w]);
-  if (c == 0 && tid == 0 && A.peak) A.peak[b] = pk;
+  if (c0 == 0 && tid == 0 && A.peak) A.peak[b] = pk;
   const float scale = 1.0f / (pk + A.norm_eps);
-  if (c >= 1) {
+  for (int c = max(c0, 1); c < cend; ++c) {
     const long long j = (long long)kChunk * c - 1;
     for (int m = tid; m < H; m += NT) outb[j * H + m] = boundary(c, m) * scale;
   }
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int i = tid + u * NT;
-    if (i < n4) {
-      float4 x = xin[u];
-      x.x *= scale; x.y *= scale; x.z *= scale; x.w *= scale;
-      o4[i] = x;
+  for (int g = 0; g < FCH; ++g) {
+    const int c = c0 + g;
+    const int j0 = kChunk * c, j1 = min(kChunk * c + kChunk - 1, T - 1);
+    float4* o4 = reinterpret_cast<float4*>(outb + (long long)j0 * H);
+    const int n4 = c < cend ? (j1 - j0) * H / 4 : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = tid + u * NT;
+      if (i < n4) {
+        float4 x = xin[g][u];
+        x.x *= scale; x.y *= scale; x.z *= scale; x.w *= scale;
+        o4[i] = x;
+      }
     }
   }
 }
@@ -1652,6 +1673,10 @@ __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
   __shared__ float red[kCThreads / 64];
   finalize_item<N>(A, blockIdx.x, A.fin_b0 + blockIdx.y, red);
 }
+
+// Grid x of the finalize kernel: FCH-chunk groups of the longest utterance.
+template <int N>
+static inline int fin_groups(int nch) { return (nch + kFinChunks<N> - 1) / kFinChunks<N>; }
 
 }  // namespace avz
 
@@ -1702,7 +1727,7 @@ static int launch_synth_rounds(const ChainArgs* a, hipStream_t st, hipEvent_t e4
   }
   ChainArgs f = *a;
   f.fin_b0 = prev_b0;
-  hipExtLaunchKernelGGL(avz_finalize_kernel<N>, dim3(nch, prev_nb), dim3(kCThreads), 0, st, e6,
+  hipExtLaunchKernelGGL(avz_finalize_kernel<N>, dim3(fin_groups<N>(nch), prev_nb), dim3(kCThreads), 0, st, e6,
                         e7, 0, f);
   return 0;
 }
@@ -1900,7 +1925,8 @@ static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
   } else {
     if (launch_synthesis<N, PF>(&s, st, nullptr, nullptr) != 0) return -3;
   }
-  hipLaunchKernelGGL(avz_finalize_kernel<N>, dim3(nch, a->batch), dim3(kCThreads), 0, st, s);
+  hipLaunchKernelGGL(avz_finalize_kernel<N>, dim3(fin_groups<N>(nch), a->batch), dim3(kCThreads), 0,
+                     st, s);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
