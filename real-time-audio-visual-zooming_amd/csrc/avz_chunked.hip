@@ -55,6 +55,11 @@ namespace avz {
 // The chain's finalize folded into the synthesis kernel: the last chunk item of an
 // utterance to finish (arrival ticket) writes its seams and peak and, for peak
 // normalisation, rescales the utterance in place (fused_finalize).
+// N = 1024 synthesis FFTs with the factored register twiddles (Fft1024x2::forward_ab)
+// instead of the block's LDS table
+#ifndef AVZ_SYN_TWAB
+#define AVZ_SYN_TWAB 0
+#endif
 #ifndef AVZ_FUSED_FIN
 #define AVZ_FUSED_FIN 0
 #endif
@@ -251,7 +256,7 @@ __device__ __forceinline__ void window_fft_pre(cf (&v)[KCfg<N>::PPL], const floa
   static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
 }
 
-template <int N>
+template <int N, bool TWAB = false>
 __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<N>& wc,
                                            const typename KCfg<N>::Fft& fft, cf* spec,
                                            const cf* twid, const LaneMap<N>& lm) {
@@ -261,7 +266,10 @@ __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<
   opaque(ac);
   opaque(as);
   window_apply<N>(v, a0, ac, as);
-  fft.forward(v, spec, twid);
+  if constexpr (TWAB)
+    fft.forward_ab(v, spec);
+  else
+    fft.forward(v, spec, twid);
   static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
 }
 
@@ -923,6 +931,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   // (INV2) or four 64-lane x1 transforms. The spectrum input path (SPEC) keeps INV2.
   constexpr bool HALF = N == 1024 && !AVZ_X1 && AVZ_SYN_HALF && !SPEC;
   constexpr bool INV2 = N == 1024 && !AVZ_X1 && AVZ_SYN_INV2 && !HALF;
+  constexpr bool TWAB = N == 1024 && !AVZ_X1 && AVZ_SYN_TWAB && !AVZ_SYN_PREWIN;
 
   cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
   float* red = reinterpret_cast<float*>(lds + G::MISC_OFF);
@@ -1087,11 +1096,12 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
                             twid, lm);
       }
 #else
-      window_fft<N>(v, wc, fft, my_spec, twid, lm);
+      window_fft<N, TWAB>(v, wc, fft, my_spec, twid, lm);
       if constexpr (G::R > 1) {
 #pragma unroll
         for (int q = 1; q < G::R; ++q)
-          window_fft<N>(vq[q - 1], wc, fft, slot_ptr<N>(lds, my_slot + q * RSTRIDE), twid, lm);
+          window_fft<N, TWAB>(vq[q - 1], wc, fft, slot_ptr<N>(lds, my_slot + q * RSTRIDE), twid,
+                              lm);
       }
 #endif
       // x2 with the x1 inverse: the next step's loads fly through apply, inverse FFT and
@@ -1371,7 +1381,10 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       cf* Zi = slot_ptr<N>(lds, 2 * p);
       auto inverse = [&](cf (&u)[PPL]) {
         static_for<0, PPL>([&](auto r) { u[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
-        fft.forward(u, Zi, twid);
+        if constexpr (TWAB)
+          fft.forward_ab(u, Zi);
+        else
+          fft.forward(u, Zi, twid);
         float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
         static_for<0, PPL>([&](auto k) {
           constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32

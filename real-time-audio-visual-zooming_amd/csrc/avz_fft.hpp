@@ -402,8 +402,18 @@ struct Fft1024x2 {
   static constexpr int TS = AVZ_TSTRIDE;
   static constexpr int GROUP_BYTES = 32 * TS * 8;
   int l;
+  // Factored stage-1 twiddles W1024^{l k}, k = 8 m + j: twa[j - 1] = W^{l j} (j < 8),
+  // twb[m - 1] = W^{8 l m} (m < 4) — 20 VGPRs in place of the 62 of a full register table
+  // or 31 LDS reads per transform (forward_ab; the synthesis kernel)
+  cf twa[7], twb[3];
 
-  __device__ __forceinline__ void init(int lane) { l = lane & 31; }
+  __device__ __forceinline__ void init(int lane) {
+    l = lane & 31;
+#pragma unroll
+    for (int j = 1; j < 8; ++j) twa[j - 1] = unit_root((double)(l * j) / N);
+#pragma unroll
+    for (int m = 1; m < 4; ++m) twb[m - 1] = unit_root((double)(8 * l * m) / N);
+  }
 
   // Fill the block-shared twiddle table tw[k1 * 32 + l] = W1024^{l k1}.
   __device__ static void fill_twiddles(cf* tw, int tid, int nthreads) {
@@ -466,6 +476,25 @@ struct Fft1024x2 {
     __builtin_amdgcn_wave_barrier();
   }
   __device__ __forceinline__ void stage2(cf (&v)[32]) const { dft32(v); }
+  // stage 1 with the factored twiddles: W^{l (8 m + j)} v = W^{8 l m} (W^{l j} v)
+  __device__ __forceinline__ void stage1_ab(cf (&v)[32]) const {
+    dft32(v);
+    static_for<1, 32>([&](auto k) {
+      constexpr int j = k & 7, m = k >> 3;
+      if constexpr (m == 0) {
+        v[k] = c_mul(v[k], twa[j - 1]);
+      } else if constexpr (j == 0) {
+        v[k] = c_mul(v[k], twb[m - 1]);
+      } else {
+        v[k] = c_mul(c_mul(v[k], twa[j - 1]), twb[m - 1]);
+      }
+    });
+  }
+  __device__ __forceinline__ void forward_ab(cf (&v)[32], cf* scratch) const {
+    stage1_ab(v);
+    transpose(v, scratch);
+    stage2(v);
+  }
   __device__ __forceinline__ void forward(cf (&v)[32], cf* scratch, const cf* tw) const {
     stage1(v, tw);
     transpose(v, scratch);
