@@ -756,7 +756,10 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysi
   KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
   const int n_items = gx * A.batch;
-  if constexpr (N == 1024 && !AVZ_X1) {
+#ifndef AVZ_IPD_TWLDS
+#define AVZ_IPD_TWLDS 0
+#endif
+  if constexpr (N == 1024 && !AVZ_X1 && !(AVZ_IPD_TWLDS && MASK == MASK_IPD)) {
     __syncthreads();
     cf tw_reg[31];
     Fft1024x2 f;
