@@ -204,13 +204,55 @@ __device__ __forceinline__ void window_apply(cf (&v)[PPL], float a0, float ac, f
   });
 }
 
+#ifndef AVZ_IL1
+#define AVZ_IL1 1
+#endif
+#ifndef AVZ_SIL1  // the synthesis kernel's stage-1 stores interleaved too (no gain, off)
+#define AVZ_SIL1 0
+#endif
+#ifndef AVZ_IL_LOADS  // next-step loads issued from inside the FFT's last stage
+#define AVZ_IL_LOADS 1
+#endif
+#ifndef AVZ_SYN_IL_LOADS  // the same in the synthesis inverse (measured 74.0 -> 75.5 us: off)
+#define AVZ_SYN_IL_LOADS 0
+#endif
+#ifndef AVZ_IL2
+#define AVZ_IL2 1
+#endif
 // Window + forward FFT with the lane's twiddles in registers (N = 1024 analysis).
+// after(k) runs right after spectrum output k is stored (AVZ_IL_LOADS: the next step's
+// load into register k).
+struct NoAfter {
+  template <class K>
+  __device__ __forceinline__ void operator()(K) const {}
+};
+template <class After = NoAfter>
 __device__ __forceinline__ void window_fft_reg(cf (&v)[32], const WinCoef<1024>& wc,
                                                const Fft1024x2& fft, cf* spec,
-                                               const cf (&tw_reg)[31], const LaneMap<1024>& lm) {
+                                               const cf (&tw_reg)[31], const LaneMap<1024>& lm,
+                                               After&& after = After{}) {
   window_apply(v, wc.a0, wc.ac, wc.as);
+#if AVZ_FFT_IL
+  if constexpr (AVZ_IL1) {
+    fft.stage1_reg_st(v, spec, tw_reg);
+    fft.transpose_read(v, spec);
+  } else {
+    fft.stage1_reg(v, tw_reg);
+    fft.transpose(v, spec);
+  }
+  if constexpr (AVZ_IL2) {
+    fft.stage2_emit(v, [&](auto k, cf x) {
+      spec[lm.out0 + 32 * k] = x;
+      after(k);
+    });
+  } else {
+    fft.stage2(v);
+    static_for<0, 32>([&](auto k) { spec[lm.out0 + 32 * k] = v[k]; });
+  }
+#else
   fft.forward_reg(v, spec, tw_reg);
   static_for<0, 32>([&](auto k) { spec[lm.out0 + 32 * k] = v[k]; });
+#endif
 }
 
 // Reference pair of the IBM mask (N = 1024, register twiddles): the reference spectrum is
@@ -220,15 +262,38 @@ __device__ __forceinline__ void window_fft_reg(cf (&v)[32], const WinCoef<1024>&
 // 32 (31 - k), or 32 (32 - k) on lane 0; DC pairs with itself) and publishes the 16 bits
 // of bins l + 32 k, k < 16, as word l of the slot (bytes 0..127, below the stored bins).
 // The Nyquist bin (lane 0, k = 16) stays readable at spec[N / 2].
+template <class After = NoAfter>
 __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCoef<1024>& wc,
                                                         const Fft1024x2& fft, cf* spec,
                                                         const cf (&tw_reg)[31],
-                                                        const LaneMap<1024>& lm) {
+                                                        const LaneMap<1024>& lm,
+                                                        After&& after = After{}) {
   constexpr int N = 1024;
   window_apply(v, wc.a0, wc.ac, wc.as);
-  fft.forward_reg(v, spec, tw_reg);
   const int l = lm.out0;
+#if AVZ_FFT_IL
+  if constexpr (AVZ_IL1) {
+    fft.stage1_reg_st(v, spec, tw_reg);
+    fft.transpose_read(v, spec);
+  } else {
+    fft.stage1_reg(v, tw_reg);
+    fft.transpose(v, spec);
+  }
+  if constexpr (AVZ_IL2) {
+    fft.stage2_emit(v, [&](auto k, cf x) {
+      if constexpr (decltype(k)::value >= 16) {
+        spec[l + 32 * k] = x;
+        after(k);
+      }
+    });
+  } else {
+    fft.stage2(v);
+    static_for<16, 32>([&](auto k) { spec[l + 32 * k] = v[k]; });
+  }
+#else
+  fft.forward_reg(v, spec, tw_reg);
   static_for<16, 32>([&](auto k) { spec[l + 32 * k] = v[k]; });
+#endif
   __builtin_amdgcn_wave_barrier();
   uint32_t w = 0u;
   static_for<0, 16>([&](auto k) {
@@ -238,6 +303,7 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
     w |= (ibm_noise(v[k], zp) ? 1u : 0u) << k;
   });
   reinterpret_cast<uint32_t*>(spec)[l] = w;
+  static_for<0, 16>([&](auto k) { after(k); });  // registers 0..15 are free now
 }
 
 // window_fft with the lane's window weights precomputed (LaneConst::ww): the synthesis
@@ -266,6 +332,17 @@ __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<
   opaque(ac);
   opaque(as);
   window_apply<N>(v, a0, ac, as);
+  if constexpr (AVZ_FFT_IL && !TWAB && std::is_same<typename C::Fft, Fft1024x2>::value) {
+    if constexpr (AVZ_SIL1) {
+      fft.stage1_lds_st(v, spec, twid);
+      fft.transpose_read(v, spec);
+    } else {
+      fft.stage1(v, twid);
+      fft.transpose(v, spec);
+    }
+    fft.stage2_emit(v, [&](auto k, cf x) { spec[lm.out0 + C::OUT_STRIDE * k] = x; });
+    return;
+  }
   if constexpr (TWAB)
     fft.forward_ab(v, spec);
   else
@@ -451,6 +528,33 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     }
   };
 
+  // AVZ_IL_LOADS (register-twiddle path): the next step's loads are issued from inside the
+  // FFT's last stage, register k right after its spectrum output is stored, so their issue
+  // overlaps the butterflies; a chunk's last step loads from an empty descriptor (reads 0,
+  // no memory traffic). Frames of a next step are >= FB >= 1: no negative sample index.
+  constexpr bool IL_LOADS = AVZ_IL_LOADS && AVZ_FFT_IL && AVZ_IL2 && N == 1024 &&
+                            !std::is_same<TW, NoTw>::value;
+  const rsrc_t r_none = make_rsrc(nullptr, 0);
+  rsrc_t rn_re = r_none, rn_im = r_none;
+  int sp_next = 0;
+  auto load_reg = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    if constexpr (SHARE) {
+      if constexpr (k < 16) {
+        const int e = sp_next + 1024 * lm.grp + 32 * k;
+        v[k].x = bload_nn(rn_re, e);
+        v[k].y = bload_nn(rn_im, e);
+      } else if constexpr ((k - 16) % 2 == 0) {
+        const int e = sp_next + 512 + 32 * (k - 16) + 32 * lm.grp;
+        v[k].x = bload_nn(rn_re, e);
+        v[k].y = bload_nn(rn_im, e);
+      }
+    } else {
+      v[k].x = bload_nn(rn_re, sp_next + C::IN_STRIDE * k);
+      v[k].y = bload_nn(rn_im, sp_next + C::IN_STRIDE * k);
+    }
+  };
+
   Acc32 acc[BPT];
   uint32_t bits[BPT];
   int ipd_clear_n[BPT];  // IPD: frames the cross-product test weighted 1
@@ -499,19 +603,32 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         const bool ident = (C::FPW == 1) ? nb == 0ull : ((nb >> (32 * lm.grp)) & 0xffffffffull) == 0ull;
         if ((lane & (64 / C::FPW - 1)) == 0) lds[G::MISC_OFF + my_slot] = ident ? 1 : 0;
       }
+      if constexpr (IL_LOADS) {
+        const bool more = step + 1 < nstep;
+        rn_re = more ? r_re : r_none;
+        rn_im = more ? r_im : r_none;
+        sp_next = (t0 + (step + 1) * FB + (SHARE ? wave_frame0 : my_frame)) * H - N / 2 + lm.in0;
+      }
       if constexpr (std::is_same<TW, NoTw>::value) {
         window_fft<N>(v, wc, fft, my_spec, twid, lm);
+      } else if constexpr (REFBITS && IL_LOADS) {
+        if (ref)
+          window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm, load_reg);
+        else
+          window_fft_reg(v, wc, fft, my_spec, tw_reg, lm, load_reg);
       } else if constexpr (REFBITS) {
         if (ref)
           window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm);
         else
           window_fft_reg(v, wc, fft, my_spec, tw_reg, lm);
+      } else if constexpr (IL_LOADS) {
+        window_fft_reg(v, wc, fft, my_spec, tw_reg, lm, load_reg);
       } else {
         window_fft_reg(v, wc, fft, my_spec, tw_reg, lm);
       }
     }
     AVZ_STAMP(3);
-    if (step + 1 < nstep) issue_loads(step + 1);
+    if (!IL_LOADS && step + 1 < nstep) issue_loads(step + 1);
     AVZ_STAMP(11);
     lds_barrier();
     AVZ_STAMP(1);
@@ -935,6 +1052,8 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   constexpr bool HALF = N == 1024 && !AVZ_X1 && AVZ_SYN_HALF && !SPEC;
   constexpr bool INV2 = N == 1024 && !AVZ_X1 && AVZ_SYN_INV2 && !HALF;
   constexpr bool TWAB = N == 1024 && !AVZ_X1 && AVZ_SYN_TWAB && !AVZ_SYN_PREWIN;
+  constexpr bool SYN_IL_LOADS = AVZ_SYN_IL_LOADS && AVZ_FFT_IL && INV2 && !TWAB && !SPEC &&
+                                KCfg<N>::SYN_R == 1;
 
   cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
   float* red = reinterpret_cast<float*>(lds + G::MISC_OFF);
@@ -1384,11 +1503,38 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       cf* Zi = slot_ptr<N>(lds, 2 * p);
       auto inverse = [&](cf (&u)[PPL]) {
         static_for<0, PPL>([&](auto r) { u[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
+        float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
+        if constexpr (AVZ_FFT_IL && !TWAB && N == 1024) {
+          if constexpr (AVZ_SIL1) {
+            fft.stage1_lds_st(u, Zi, twid);
+            fft.transpose_read(u, Zi);
+          } else {
+            fft.stage1(u, twid);
+            fft.transpose(u, Zi);
+          }
+          // INV2 runs in the sample registers: the next step's load into register k is
+          // issued as soon as output k is stored (SYN_IL_LOADS; an empty descriptor after
+          // the chunk's last step)
+          const rsrc_t rz = make_rsrc(nullptr, 0);
+          const rsrc_t rn0 = more ? r_m0 : rz, rn1 = more ? r_m1 : rz;
+          const int s0n = (t0 + (step + 1) * FB + my_slot) * H - N / 2 + lm.in0;
+          fft.stage2_emit(u, [&](auto k, cf x) {
+            constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+            const float w = fmaf(wc.ss, sk, fmaf(-wc.sc, ck, wc.s0));
+            const int n = lm.out0 + C::OUT_STRIDE * k;
+            Cp[n] = x.x * w;       // frame 2p   (real part of the inverse)
+            Cp[N + n] = -x.y * w;  // frame 2p+1 (imaginary part; conjugation trick)
+            if constexpr (SYN_IL_LOADS) {
+              u[k].x = bload_nn(rn0, s0n + C::IN_STRIDE * k);
+              u[k].y = bload_nn(rn1, s0n + C::IN_STRIDE * k);
+            }
+          });
+          return;
+        }
         if constexpr (TWAB)
           fft.forward_ab(u, Zi);
         else
           fft.forward(u, Zi, twid);
-        float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
         static_for<0, PPL>([&](auto k) {
           constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
           const float w = fmaf(wc.ss, sk, fmaf(-wc.sc, ck, wc.s0));
@@ -1404,7 +1550,7 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         inverse(u);
       }
     }
-    if ((AVZ_X1 || INV2) && !SPEC && more) issue_loads(step + 1);
+    if ((AVZ_X1 || INV2) && !SPEC && more && !(SYN_IL_LOADS && ifft_wave)) issue_loads(step + 1);
     lds_barrier();
     AVZ_STAMP(8);
 

@@ -34,6 +34,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include <utility>
 
 namespace avz {
@@ -287,6 +288,31 @@ __device__ __forceinline__ void dft32(cf (&v)[32]) {
 #endif
 }
 
+// dft32 without its last radix-2 stage: e / o = 16-point DFTs of the even / odd inputs.
+// The callers run the last stage one output pair (k, k + 16) at a time and store each pair
+// as soon as it is formed (AVZ_FFT_IL), behind a scheduling fence, so the LDS stores of a
+// transpose or spectrum issue between the butterflies instead of as one burst after them.
+__device__ __forceinline__ void dft32_halves(const cf (&v)[32], cf (&e)[16], cf (&o)[16]) {
+  static_for<0, 16>([&](auto i) {
+    e[i] = v[2 * i];
+    o[i] = v[2 * i + 1];
+  });
+  dft16(e);
+  dft16(o);
+}
+#ifndef AVZ_FFT_IL
+#define AVZ_FFT_IL 1
+#endif
+#ifndef AVZ_IL1_GROUP
+#define AVZ_IL1_GROUP 99  // no fence: the scheduler interleaves these stores itself
+#endif
+#ifndef AVZ_IL_TWD
+#define AVZ_IL_TWD 2
+#endif
+#ifndef AVZ_IL1_MASK
+#define AVZ_IL1_MASK 0
+#endif
+
 __device__ __forceinline__ cf unit_root(double frac) {
   // exp(-2 pi i frac), evaluated in fp64 then rounded
   double s, c;
@@ -476,6 +502,75 @@ struct Fft1024x2 {
     __builtin_amdgcn_wave_barrier();
   }
   __device__ __forceinline__ void stage2(cf (&v)[32]) const { dft32(v); }
+
+  // ---- interleaved forms (AVZ_FFT_IL): each output pair (k, k + 16) of a stage's last
+  // radix-2 is stored the moment it is formed, one pair per scheduling group.
+  // Stage 1 with register twiddles -> transpose scratch.
+  __device__ __forceinline__ void stage1_reg_st(cf (&v)[32], cf* scratch,
+                                                const cf (&tw_reg)[31]) const {
+    cf e[16], o[16];
+    dft32_halves(v, e, o);
+    static_for<0, 16>([&](auto k) {
+      cf a, b;
+      bfly_tw<k>(e[k], o[k], a, b);
+      if constexpr (k > 0) a = c_mul(a, tw_reg[k - 1]);
+      b = c_mul(b, tw_reg[k + 15]);
+      scratch[k * TS + l] = a;
+      scratch[(k + 16) * TS + l] = b;
+      if constexpr (k % AVZ_IL1_GROUP == AVZ_IL1_GROUP - 1) __builtin_amdgcn_sched_barrier(AVZ_IL1_MASK);
+    });
+  }
+  // Stage 1 with the block's LDS twiddle table tw[k1 * 32 + l]: the two twiddles of pair k
+  // are read two pairs ahead.
+  __device__ __forceinline__ void stage1_lds_st(cf (&v)[32], cf* scratch, const cf* tw) const {
+    constexpr int D = AVZ_IL_TWD;  // read distance (pairs)
+    cf ta[D + 1], tb[D + 1];
+    static_for<0, D>([&](auto k) {
+      ta[k] = lds_read(tw + k * 32 + l);
+      tb[k] = lds_read(tw + (k + 16) * 32 + l);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    cf e[16], o[16];
+    dft32_halves(v, e, o);
+    static_for<0, 16>([&](auto k) {
+      if constexpr (k + D < 16) {
+        ta[(k + D) % (D + 1)] = lds_read(tw + (k + D) * 32 + l);
+        tb[(k + D) % (D + 1)] = lds_read(tw + (k + D + 16) * 32 + l);
+      }
+      cf a, b;
+      bfly_tw<k>(e[k], o[k], a, b);
+      if constexpr (k > 0) a = c_mul(a, ta[k % (D + 1)]);
+      b = c_mul(b, tb[k % (D + 1)]);
+      scratch[k * TS + l] = a;
+      scratch[(k + 16) * TS + l] = b;
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+  // Rows of the transpose back into registers (after a stage1_*_st).
+  __device__ __forceinline__ void transpose_read(cf (&v)[32], const cf* scratch) const {
+    __builtin_amdgcn_wave_barrier();
+    static_assert(TS % 2 == 0, "16-B rows");
+    const float4* row = reinterpret_cast<const float4*>(scratch + l * TS);
+    static_for<0, 16>([&](auto q) {
+      const float4 x = row[q];
+      v[2 * q] = cf{x.x, x.y};
+      v[2 * q + 1] = cf{x.z, x.w};
+    });
+    __builtin_amdgcn_wave_barrier();
+  }
+  // Stage 2 with emit(k, X[l + 32 k]) called for both outputs of each pair as it is formed
+  // (v keeps the outputs, as stage2).
+  template <class Emit>
+  __device__ __forceinline__ void stage2_emit(cf (&v)[32], Emit&& emit) const {
+    cf e[16], o[16];
+    dft32_halves(v, e, o);
+    static_for<0, 16>([&](auto k) {
+      bfly_tw<k>(e[k], o[k], v[k], v[k + 16]);
+      emit(k, v[k]);
+      emit(std::integral_constant<int, k + 16>{}, v[k + 16]);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
   // stage 1 with the factored twiddles: W^{l (8 m + j)} v = W^{8 l m} (W^{l j} v)
   __device__ __forceinline__ void stage1_ab(cf (&v)[32]) const {
     dft32(v);
