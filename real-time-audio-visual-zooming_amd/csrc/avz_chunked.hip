@@ -213,6 +213,9 @@ __device__ __forceinline__ void window_apply(cf (&v)[PPL], float a0, float ac, f
 #ifndef AVZ_IL_LOADS  // next-step loads issued from inside the FFT's last stage
 #define AVZ_IL_LOADS 1
 #endif
+#ifndef AVZ_REF_ALL  // IBM reference waves store all 32 outputs (loads interleaved for all)
+#define AVZ_REF_ALL 1
+#endif
 #ifndef AVZ_SYN_IL_LOADS  // the same in the synthesis inverse (measured 74.0 -> 75.5 us: off)
 #define AVZ_SYN_IL_LOADS 0
 #endif
@@ -279,7 +282,25 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
     fft.stage1_reg(v, tw_reg);
     fft.transpose(v, spec);
   }
-  if constexpr (AVZ_IL2) {
+  if constexpr (AVZ_IL2 && AVZ_REF_ALL) {
+    // all 32 outputs stored, so every register takes its next-step load during the stage
+    // (the lower half is read back below instead of being held for the bits)
+    fft.stage2_emit(v, [&](auto k, cf x) {
+      spec[l + 32 * k] = x;
+      after(k);
+    });
+    __builtin_amdgcn_wave_barrier();
+    uint32_t w = 0u;
+    cf zo[16], zp[16];
+    static_for<0, 16>([&](auto k) {
+      const int m = l + 32 * k;
+      zo[k] = spec[m];
+      zp[k] = spec[(N - m) & (N - 1)];
+    });
+    static_for<0, 16>([&](auto k) { w |= (ibm_noise(zo[k], zp[k]) ? 1u : 0u) << k; });
+    reinterpret_cast<uint32_t*>(spec)[l] = w;
+    return;
+  } else if constexpr (AVZ_IL2) {
     fft.stage2_emit(v, [&](auto k, cf x) {
       if constexpr (decltype(k)::value >= 16) {
         spec[l + 32 * k] = x;
@@ -322,10 +343,13 @@ __device__ __forceinline__ void window_fft_pre(cf (&v)[KCfg<N>::PPL], const floa
   static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
 }
 
-template <int N, bool TWAB = false>
+// IL512: the interleaved Fft512x2 (the synthesis kernel at two blocks per CU: 81.0 -> 80.3
+// us; the three-block N = 512 analysis kernel ran slower with it, 81.3 -> 82.5 us)
+template <int N, bool TWAB = false, bool IL512 = false, class After = NoAfter>
 __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<N>& wc,
                                            const typename KCfg<N>::Fft& fft, cf* spec,
-                                           const cf* twid, const LaneMap<N>& lm) {
+                                           const cf* twid, const LaneMap<N>& lm,
+                                           After&& after = After{}) {
   using C = KCfg<N>;
   float a0 = wc.a0, ac = wc.ac, as = wc.as;
   opaque(a0);
@@ -341,6 +365,13 @@ __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<
       fft.transpose(v, spec);
     }
     fft.stage2_emit(v, [&](auto k, cf x) { spec[lm.out0 + C::OUT_STRIDE * k] = x; });
+    return;
+  }
+  if constexpr (AVZ_FFT_IL && IL512 && std::is_same<typename C::Fft, Fft512x2>::value) {
+    fft.forward_emit(v, spec, [&](auto k, cf x) {
+      spec[lm.out0 + C::OUT_STRIDE * k] = x;
+      after(k);
+    });
     return;
   }
   if constexpr (TWAB)
@@ -1218,11 +1249,11 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
                             twid, lm);
       }
 #else
-      window_fft<N, TWAB>(v, wc, fft, my_spec, twid, lm);
+      window_fft<N, TWAB, true>(v, wc, fft, my_spec, twid, lm);
       if constexpr (G::R > 1) {
 #pragma unroll
         for (int q = 1; q < G::R; ++q)
-          window_fft<N, TWAB>(vq[q - 1], wc, fft, slot_ptr<N>(lds, my_slot + q * RSTRIDE), twid,
+          window_fft<N, TWAB, true>(vq[q - 1], wc, fft, slot_ptr<N>(lds, my_slot + q * RSTRIDE), twid,
                               lm);
       }
 #endif
@@ -1528,6 +1559,16 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
               u[k].x = bload_nn(rn0, s0n + C::IN_STRIDE * k);
               u[k].y = bload_nn(rn1, s0n + C::IN_STRIDE * k);
             }
+          });
+          return;
+        }
+        if constexpr (AVZ_FFT_IL && N == 512) {
+          fft.forward_emit(u, Zi, [&](auto k, cf x) {
+            constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+            const float w = fmaf(wc.ss, sk, fmaf(-wc.sc, ck, wc.s0));
+            const int n = lm.out0 + C::OUT_STRIDE * k;
+            Cp[n] = x.x * w;       // frame 2p   (real part of the inverse)
+            Cp[N + n] = -x.y * w;  // frame 2p+1 (imaginary part; conjugation trick)
           });
           return;
         }

@@ -29,12 +29,15 @@ __device__ __forceinline__ float bload(rsrc_t r, int elem) {
 // Diagnostic build only (-DAVZ_STAMPS): wave 0 accumulates s_memrealtime (100 MHz)
 // deltas per phase into g_stamps[linear block id][16] (phase lists: tools/phase_profile.py).
 #ifdef AVZ_STAMPS
+#ifndef AVZ_STAMP_WAVE  // the wave whose lane 0 stamps
+#define AVZ_STAMP_WAVE 0
+#endif
 static __device__ unsigned long long* g_stamps;
 #define AVZ_STAMP_DECL() unsigned long long stamp_prev = 0
 #define AVZ_STAMP_INIT() stamp_prev = __builtin_amdgcn_s_memrealtime()
 #define AVZ_STAMP(i)                                                        \
   do {                                                                      \
-    if (threadIdx.x == 0 && g_stamps) {                                     \
+    if (threadIdx.x == 64 * AVZ_STAMP_WAVE && g_stamps) {                   \
       const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();     \
       atomicAdd(g_stamps + (blockIdx.y * gridDim.x + blockIdx.x) * 16 + (i), now_ - stamp_prev); \
       stamp_prev = now_;                                                    \

@@ -219,6 +219,21 @@ __device__ __forceinline__ void dft16(cf (&v)[16]) {
   static_for<0, 16>([&](auto i) { v[i] = t[i]; });
 }
 
+// dft16 with emit(k, X[k]) called for the four outputs of each last-stage 4-point DFT as
+// they are formed (AVZ_FFT_IL; v is left holding the last stage's inputs).
+template <class Emit>
+__device__ __forceinline__ void dft16_emit(cf (&v)[16], Emit&& emit) {
+  static_for<0, 4>([&](auto n2) { dft4(v[n2], v[n2 + 4], v[n2 + 8], v[n2 + 12]); });
+  static_for<0, 4>([&](auto k1) {
+    cf a0 = v[0 + 4 * k1], a1 = v[1 + 4 * k1], a2 = v[2 + 4 * k1], a3 = v[3 + 4 * k1];
+    dft4_tw<2 * k1>(a0, a1, a2, a3);
+    emit(std::integral_constant<int, k1 + 0>{}, a0);
+    emit(std::integral_constant<int, k1 + 4>{}, a1);
+    emit(std::integral_constant<int, k1 + 8>{}, a2);
+    emit(std::integral_constant<int, k1 + 12>{}, a3);
+  });
+}
+
 // Cross-lane exchange between the two halves of a lane pair at distance DIST
 // (32: lanes l / l+32 via v_permlane32_swap; 16: rows 2g / 2g+1 via
 // v_permlane16_swap). Returns (value of the lower partner, value of the upper).
@@ -240,8 +255,13 @@ __device__ __forceinline__ void xhalf(float v, float& lo, float& hi) {
 // Radix-2 DIT butterfly across lane halves after both halves ran dft16 on their
 // even (h=0) / odd (h=1) inputs: out[k'] = E[k'] + sgn * W32^{k'} O[k'],
 // sgn = +1 on the lower half (bin k'), -1 on the upper half (bin k'+16).
-template <int DIST>
-__device__ __forceinline__ void xhalf_dit(cf (&v)[16], float sgn) {
+struct NoEmit {
+  template <class K>
+  __device__ __forceinline__ void operator()(K, cf) const {}
+};
+template <int DIST, class Emit = NoEmit>
+__device__ __forceinline__ void xhalf_dit(cf (&v)[16], float sgn, Emit&& emit = Emit{}) {
+  constexpr bool EMIT = !std::is_same<std::decay_t<Emit>, NoEmit>::value;
   static_for<0, 16>([&](auto k) {
     float ex, ox, ey, oy;
     xhalf<DIST>(v[k].x, ex, ox);
@@ -265,6 +285,10 @@ __device__ __forceinline__ void xhalf_dit(cf (&v)[16], float sgn) {
     const cf t = w32mul<k>(cf{ox, oy});
     v[k] = {fmaf(sgn, t.x, ex), fmaf(sgn, t.y, ey)};
 #endif
+    if constexpr (EMIT) {
+      emit(k, v[k]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   });
 }
 
@@ -305,6 +329,9 @@ __device__ __forceinline__ void dft32_halves(const cf (&v)[32], cf (&e)[16], cf 
 #endif
 #ifndef AVZ_IL1_GROUP
 #define AVZ_IL1_GROUP 99  // no fence: the scheduler interleaves these stores itself
+#endif
+#ifndef AVZ_SIL1_FENCE
+#define AVZ_SIL1_FENCE 1
 #endif
 #ifndef AVZ_IL_TWD
 #define AVZ_IL_TWD 2
@@ -543,7 +570,7 @@ struct Fft1024x2 {
       b = c_mul(b, tb[k % (D + 1)]);
       scratch[k * TS + l] = a;
       scratch[(k + 16) * TS + l] = b;
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (AVZ_SIL1_FENCE) __builtin_amdgcn_sched_barrier(0);
     });
   }
   // Rows of the transpose back into registers (after a stage1_*_st).
@@ -623,6 +650,21 @@ struct Fft512x2 {
   }
 
   __device__ static void fill_twiddles(cf*, int, int) {}
+
+  // forward with the transpose stores issued as stage 1's outputs are formed and emit(k,
+  // X_g[k1 + 16 k + 256 h]) called for each output of stage 2 as it is formed (AVZ_FFT_IL)
+  template <class Emit>
+  __device__ __forceinline__ void forward_emit(cf (&v)[16], cf* scratch, Emit&& emit) const {
+    dft16_emit(v, [&](auto k, cf x) {
+      if constexpr (decltype(k)::value > 0) x = c_mul(x, tw[k - 1]);
+      scratch[k * 34 + j] = x;
+    });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = scratch[k1 * 34 + 2 * r + h2]; });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<16>(v, sgn, emit);
+  }
 
   // v: x_g[j + 32 r] in; X_g[k1 + 16 r + 256 h] out. scratch: this lane group's slot.
   __device__ __forceinline__ void forward(cf (&v)[16], cf* scratch, const cf* = nullptr) const {

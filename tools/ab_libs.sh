@@ -16,6 +16,6 @@ fi
 for rep in $(seq 1 ${REPS:-2}); do
 for lib in "$@"; do
   AVZ_LIB=$D/$lib timeout -k 10 200 python bench.py --no-cpu ${BENCH_ARGS} > $out/bench_${lib}_$rep.log 2>&1 || { tail -20 $out/bench_${lib}_$rep.log; exit 1; }
-  tail -1 $out/bench_${lib}_$rep.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(sys.argv[1], round(d["value"]/1e9,2), "G ms/step", round(d["ms_per_step"],4), {k: round(v*1e3,1) for k,v in r.get("kernels_ms",{}).items()})' $lib
+  tail -1 $out/bench_${lib}_$rep.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(sys.argv[1], round(d["value"]/1e9,2), "G ms/step", round(d["ms_per_step"],4), {k: round(v*1e3,1) for k,v in r.get("kernels_ms",{}).items()}, "dominant", round(r.get("dominant_kernel",{}).get("kernel_ms",0)*1e3,1))' $lib
 done
 done
