@@ -55,10 +55,11 @@ namespace avz {
 // The chain's finalize folded into the synthesis kernel: the last chunk item of an
 // utterance to finish (arrival ticket) writes its seams and peak and, for peak
 // normalisation, rescales the utterance in place (fused_finalize).
-// N = 1024 synthesis FFTs with the factored register twiddles (Fft1024x2::forward_ab)
-// instead of the block's LDS table
+// N = 1024 synthesis FFTs with the factored register twiddles (Fft1024x2::stage1_ab_st,
+// stage-1 pairs stored as formed) instead of the block's LDS table: synthesis 73.7-74.1 ->
+// 72.7-73.1 us (profiles/r03d/ab_more.txt r03n2); before the interleaved stores it was neutral
 #ifndef AVZ_SYN_TWAB
-#define AVZ_SYN_TWAB 0
+#define AVZ_SYN_TWAB 1
 #endif
 #ifndef AVZ_FUSED_FIN
 #define AVZ_FUSED_FIN 0
@@ -369,6 +370,15 @@ __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<
   }
   if constexpr (AVZ_FFT_IL && IL512 && std::is_same<typename C::Fft, Fft512x2>::value) {
     fft.forward_emit(v, spec, [&](auto k, cf x) {
+      spec[lm.out0 + C::OUT_STRIDE * k] = x;
+      after(k);
+    });
+    return;
+  }
+  if constexpr (AVZ_FFT_IL && TWAB && std::is_same<typename C::Fft, Fft1024x2>::value) {
+    fft.stage1_ab_st(v, spec);
+    fft.transpose_read(v, spec);
+    fft.stage2_emit(v, [&](auto k, cf x) {
       spec[lm.out0 + C::OUT_STRIDE * k] = x;
       after(k);
     });
@@ -1535,8 +1545,11 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       auto inverse = [&](cf (&u)[PPL]) {
         static_for<0, PPL>([&](auto r) { u[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
         float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
-        if constexpr (AVZ_FFT_IL && !TWAB && N == 1024) {
-          if constexpr (AVZ_SIL1) {
+        if constexpr (AVZ_FFT_IL && N == 1024) {
+          if constexpr (TWAB) {
+            fft.stage1_ab_st(u, Zi);
+            fft.transpose_read(u, Zi);
+          } else if constexpr (AVZ_SIL1) {
             fft.stage1_lds_st(u, Zi, twid);
             fft.transpose_read(u, Zi);
           } else {

@@ -547,6 +547,24 @@ struct Fft1024x2 {
       if constexpr (k % AVZ_IL1_GROUP == AVZ_IL1_GROUP - 1) __builtin_amdgcn_sched_barrier(AVZ_IL1_MASK);
     });
   }
+  // Stage 1 with the factored register twiddles (forward_ab's), pairs stored as formed.
+  __device__ __forceinline__ void stage1_ab_st(cf (&v)[32], cf* scratch) const {
+    cf e[16], o[16];
+    dft32_halves(v, e, o);
+    auto tw = [&](auto kc, cf x) {
+      constexpr int k = decltype(kc)::value, j = k & 7, m = k >> 3;
+      if constexpr (k == 0) return x;
+      else if constexpr (m == 0) return c_mul(x, twa[j - 1]);
+      else if constexpr (j == 0) return c_mul(x, twb[m - 1]);
+      else return c_mul(c_mul(x, twa[j - 1]), twb[m - 1]);
+    };
+    static_for<0, 16>([&](auto k) {
+      cf a, b;
+      bfly_tw<k>(e[k], o[k], a, b);
+      scratch[k * TS + l] = tw(k, a);
+      scratch[(k + 16) * TS + l] = tw(std::integral_constant<int, k + 16>{}, b);
+    });
+  }
   // Stage 1 with the block's LDS twiddle table tw[k1 * 32 + l]: the two twiddles of pair k
   // are read two pairs ahead.
   __device__ __forceinline__ void stage1_lds_st(cf (&v)[32], cf* scratch, const cf* tw) const {
