@@ -327,17 +327,11 @@ __device__ __forceinline__ void dft32_halves(const cf (&v)[32], cf (&e)[16], cf 
 #ifndef AVZ_FFT_IL
 #define AVZ_FFT_IL 1
 #endif
-#ifndef AVZ_IL1_GROUP
-#define AVZ_IL1_GROUP 99  // no fence: the scheduler interleaves these stores itself
-#endif
 #ifndef AVZ_SIL1_FENCE
 #define AVZ_SIL1_FENCE 1
 #endif
 #ifndef AVZ_IL_TWD
 #define AVZ_IL_TWD 2
-#endif
-#ifndef AVZ_IL1_MASK
-#define AVZ_IL1_MASK 0
 #endif
 
 __device__ __forceinline__ cf unit_root(double frac) {
@@ -544,7 +538,8 @@ struct Fft1024x2 {
       b = c_mul(b, tw_reg[k + 15]);
       scratch[k * TS + l] = a;
       scratch[(k + 16) * TS + l] = b;
-      if constexpr (k % AVZ_IL1_GROUP == AVZ_IL1_GROUP - 1) __builtin_amdgcn_sched_barrier(AVZ_IL1_MASK);
+      // no scheduling fence: the compiler spreads these stores over the butterflies by
+      // itself (a fence per pair or per 2-4 pairs made it spill 88-152 B)
     });
   }
   // Stage 1 with the factored register twiddles (forward_ab's), pairs stored as formed.
