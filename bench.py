@@ -52,6 +52,7 @@ import numpy as np  # noqa: E402
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 FS, SECONDS = 16000, 4.0
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md, FP32 vector / matrix peak (spec)
 DEFAULT_BATCH = {"ibm": 256, "ipd": 1024, "unet": 1024}
 CPU_SHARE = 16  # host cores per GPU on the MI355X boxes (their CPU share; nproc shows the machine)
 WORKLOAD_TEXT = {
@@ -173,6 +174,7 @@ def cpu_baseline(sample, seconds, workers, workload, n_fft, available):
 
 # ----------------------------------------------------------------------------- workloads
 TIMING_PERIOD = 4  # timed steps per HIP-event-bracketed analysis launch
+UNET_SECONDARY_STEPS = 2  # configs[4] end to end in the default run: ~1.4 s per step
 SETTLE_BLOCK = 20  # steps per clock-settling block
 SETTLE_MIN_S = 0.1  # sustained load before the convergence test (the clock ramps for tens of ms)
 SETTLE_MAX_S = 0.6  # cap on the settling phase
@@ -266,6 +268,56 @@ def setup_unet(spec, dev, batches, unet_dtype):
                 alg_chain=n_items * (2 * bf.chunk * 4 + n_out * 4),
                 kernel=f"avz_analysis_kernel<{n_fft},EXTERNAL>", mix=batches[0][0], y=y, it=it)
     return step, info
+
+
+def conv_flops(model, x):
+    """FLOPs of one forward of `model` on x (2 per multiply-add of every Conv2d /
+    ConvTranspose2d, counted by hooks on a forward of x)."""
+    import torch
+    tot = [0]
+
+    def hook(mod, inp, out):
+        k = mod.weight.shape  # Conv2d [cout, cin/g, kh, kw]; ConvTranspose2d [cin, cout/g, kh, kw]
+        if isinstance(mod, torch.nn.ConvTranspose2d):
+            tot[0] += 2 * inp[0].numel() * k[1] * k[2] * k[3]
+        else:
+            tot[0] += 2 * out.numel() * k[1] * k[2] * k[3]
+    hs = [m.register_forward_hook(hook) for m in model.modules()
+          if isinstance(m, (torch.nn.Conv2d, torch.nn.ConvTranspose2d))]
+    with torch.no_grad():
+        model(x)
+    for h in hs:
+        h.remove()
+    return tot[0]
+
+
+def unet_figures(info, K, chain_ms):
+    """configs[4]'s parts, timed alone on the same items: the U-Net forward (device features
+    included) with its achieved TFLOP/s against the fp32 peak, and the MVDR chain."""
+    import torch
+    bf = info["bf"]
+    items = bf.split(info["mix"])[0]
+    from avz import neural as N
+    x = N.mask_features(bf.plan, items[:1], "unet")
+    if bf.channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
+    flops_chunk = conv_flops(bf.model, x)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = max(1, K // 2)
+    e0.record()
+    for _ in range(n):
+        bf.masks(items)
+    e1.record()
+    torch.cuda.synchronize()
+    unet_ms = e0.elapsed_time(e1) / n
+    tflops = flops_chunk * info["n_items"] / (unet_ms * 1e-3) / 1e12
+    return {"unet_ms": unet_ms, "mvdr_chain_ms": chain_ms,
+            "mvdr_chain_tf_bins_per_s": info["bins"] / (chain_ms * 1e-3),
+            "unet_gflop_per_chunk": flops_chunk / 1e9, "unet_tflops": tflops,
+            "unet_frac_fp32_peak": tflops / FP32_PEAK_TFLOPS,
+            "unet_note": ("U-Net forward incl. device features, torch events around masks() on "
+                          "the batch's chunk items; FLOPs = 2 x MACs of every convolution")}
 
 
 def setup_chain4(spec, dev, batches):
@@ -444,7 +496,7 @@ def main():
     import torch.distributed as dist
 
     from avz import metrics
-    from avz.batch_run import allreduce_job
+    from avz.batch_run import allreduce_job, finite_sums
     from oracle import avz_oracle as O
 
     # --rehearse-shared-gpu: every rank on cuda:0 with gloo, to exercise the N > 1 code
@@ -485,18 +537,7 @@ def main():
 
     extra = {}
     if args.workload == "unet":  # the U-Net forward alone (features included), same items
-        bf = info["bf"]
-        items = bf.split(info["mix"])[0]
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(max(1, K // 2)):
-            bf.masks(items)
-        e1.record()
-        torch.cuda.synchronize()
-        extra["unet_ms"] = e0.elapsed_time(e1) / max(1, K // 2)
-        extra["mvdr_chain_ms"] = chain_ms
-        extra["mvdr_chain_tf_bins_per_s"] = info["bins"] / (chain_ms * 1e-3)
+        extra.update(unet_figures(info, K, chain_ms))
 
     if args.workload != "unet" and rank == 0:
         try:
@@ -548,8 +589,9 @@ def main():
     m = metrics.projection_metrics(est, torch.cat([d_tgt] * 2), torch.cat([d_itf] * 2),
                                    est_peak=est_peak)
     sir_out, sir_in = m[:B, 3], m[B:, 3]
-    sums = torch.stack([sir_in.sum(), sir_out.sum(), torch.tensor(float(B), device=dev,
-                                                                  dtype=torch.float64)])
+    # [sum SIR_in, sum SIR_out, sum OSINR_out, n_ok, n] over the utterances
+    # whose metrics are finite (batch_run.finite_sums)
+    sums = finite_sums([sir_in, sir_out, m[:B, 0]], B)
     if world > 1:  # SUM of the metric sums, MAX over ranks of the timings
         kn = plan.KERNELS + ("analysis_timed",)
         mx = torch.tensor([elapsed_s, step_ms, chain_ms] + ([kt[k] for k in kn] if kt else []),
@@ -635,6 +677,9 @@ def main():
                                         "(un-normalised output + peak[B])")),
             ("configs[4]_chain", dict(workload="chain4", B=1024, k=2, n_fft=1024, normalize="none",
                                       text=WORKLOAD_TEXT["chain4"].format(B=1024, n=1024, h=512))),
+            ("configs[4]_unet", dict(workload="unet", B=1024, k=2, n_fft=1024, normalize="none",
+                                     text=WORKLOAD_TEXT["unet"].format(B=1024, unet_dtype="fp32",
+                                                                       n=1024, h=512))),
         ]
         try:  # the spectral-domain operator on a 4096-item chunk batch (configs[4]'s items)
             st, inf = setup_spectral(4096, dev, n_sets)
@@ -660,13 +705,24 @@ def main():
         for name, sp in specs:
             try:
                 bs = [gen_batch(sp, dev, i * sp["B"], args.scenes) for i in range(n_sets)]
-                if sp["workload"] == "chain4":
+                if sp["workload"] == "unet":
+                    # one U-Net step takes ~1.3-1.4 s: a few steps, no settling blocks
+                    Ku = UNET_SECONDARY_STEPS
+                    st, inf = setup_unet(sp, dev, bs, "fp32")
+                    el, ktx, _ = run_timed(st, inf["plan"], Ku, 1, 1, dev, False,
+                                           not args.no_kernel_timing)
+                    cm = sum(ktx[k] for k in inf["plan"].KERNELS) if ktx else 1e3 * el / Ku
+                    secondary[name] = secondary_entry(sp, inf, Ku, el, ktx, 1)
+                    secondary[name].update(unet_figures(inf, Ku, cm))
+                    secondary[name]["steps"] = Ku
+                elif sp["workload"] == "chain4":
                     st, inf = setup_chain4(sp, dev, bs)
                 else:
                     st, inf = setup_chain(sp, dev, bs)
-                el, ktx, _ = run_timed(st, inf["plan"], K, args.warmup, 1, dev,
-                                       not args.no_settle, not args.no_kernel_timing)
-                secondary[name] = secondary_entry(sp, inf, K, el, ktx, 1)
+                if sp["workload"] != "unet":
+                    el, ktx, _ = run_timed(st, inf["plan"], K, args.warmup, 1, dev,
+                                           not args.no_settle, not args.no_kernel_timing)
+                    secondary[name] = secondary_entry(sp, inf, K, el, ktx, 1)
                 del bs, st, inf
                 torch.cuda.empty_cache()
             except Exception as exc:  # a side figure must never sink the bench line
@@ -707,9 +763,11 @@ def main():
             "config": cfg,
             "roofline": roof,
             "cpu_baseline": cpu,
-            "sir": {"sir_in_mean_db": float(sums[0] / sums[2]),
-                    "sir_out_mean_db": float(sums[1] / sums[2]),
-                    "sir_abs_delta_vs_reference_db": d_sir, "n_utts": int(sums[2])},
+            "sir": {"sir_in_mean_db": float(sums[0] / max(float(sums[3]), 1.0)),
+                    "sir_out_mean_db": float(sums[1] / max(float(sums[3]), 1.0)),
+                    "osinr_out_mean_db": float(sums[2] / max(float(sums[3]), 1.0)),
+                    "sir_abs_delta_vs_reference_db": d_sir, "n_ok": int(sums[3]),
+                    "n_utts": int(sums[4])},
         }
         line.update(extra)
         if secondary is not None:

@@ -56,10 +56,26 @@ def world_info():
     return 0, 1
 
 
+def finite_sums(cols, n=None):
+    """SURVEY 8(e)'s metric sums with a non-finite guard, on the device: [sum of each
+    column over the utterances whose every column is finite, n_ok(, n)]. One utterance with
+    a NaN / inf metric (an all-zero output scores 0/0) would otherwise poison the global
+    mean; the reference isolates such items per run (Final_pipeline/batch_run.py:47-49,
+    its CSV row still written, metrics.py:102-123)."""
+    x = torch.stack([c.double() for c in cols])
+    ok = torch.isfinite(x).all(0)
+    out = [torch.where(ok, x, torch.zeros_like(x)).sum(1), ok.sum().double()[None]]
+    if n is not None:
+        out.append(torch.full((1,), float(n), dtype=torch.float64, device=x.device))
+    return torch.cat(out)
+
+
 @dataclass
 class BatchResult:
     rows: list            # this rank's CSV rows
-    sums: np.ndarray      # global [sum OSIR_in, sum OSIR_out, sum OSINR_in, sum OSINR_out, n]
+    # global [sum OSIR_in, sum OSIR_out, sum OSINR_in, sum OSINR_out, n_ok, n]; the sums
+    # run over the n_ok utterances whose four metrics are finite
+    sums: np.ndarray
 
     @property
     def mean_sir_improvement(self):
@@ -103,7 +119,7 @@ def run_batch(n_runs: int, start_idx: int = 0, n_interferers: int = 2, *,
     if enhance is None:
         enhance = gpu_enhancer(max_batch=batch, max_samples=S, device=dev)
     rows = []
-    sums = torch.zeros(5, dtype=torch.float64, device=dev)
+    sums = torch.zeros(6, dtype=torch.float64, device=dev)
     for c0 in range(start_idx + lo, start_idx + hi, batch):
         nb = min(batch, start_idx + hi - c0)
         if scenes == "philox" and dev.type == "cuda":
@@ -124,15 +140,14 @@ def run_batch(n_runs: int, start_idx: int = 0, n_interferers: int = 2, *,
         osinr_b, osir_b = metrics.calculate_osnr_osir(d_mix[:, 0, :L], d_tgt[:, :L], d_itf[:, :L])
         osinr_s, osir_s = metrics.calculate_osnr_osir(out[:, :L], d_tgt[:, :L], d_itf[:, :L],
                                                       peak=peak)
-        sums += torch.stack([osir_b.sum(), osir_s.sum(), osinr_b.sum(), osinr_s.sum(),
-                             torch.tensor(float(nb), dtype=torch.float64, device=dev)])
+        sums += finite_sums([osir_b, osir_s, osinr_b, osinr_s], nb)
         vals = torch.stack([osir_b, osir_s, osinr_b, osinr_s]).cpu().numpy()
         for j in range(nb):
             rows.append({"Run_ID": f"batch_test_{c0 + j:03d}", "SIR_Base": f"{vals[0, j]:.2f}",
                          "SIR_Enh": f"{vals[1, j]:.2f}", "SIR_Imp": f"{vals[1, j] - vals[0, j]:.2f}",
                          "SINR_Base": f"{vals[2, j]:.2f}", "SINR_Enh": f"{vals[3, j]:.2f}",
                          "STOI": "0.0000", "PESQ_WB": "0.0000", "PESQ_NB": "0.0000"})
-    allreduce_job(sums)  # the only collective: metric sums
+    allreduce_job(sums)  # the only collective: metric sums (+ n_ok, n)
     if csv_path is not None:
         append_csv(csv_path, rows, rank, world)
     return BatchResult(rows=rows, sums=sums.cpu().numpy())

@@ -22,7 +22,6 @@ struct Workspace {
   float* heads;
   float* tails;
   uint32_t* peak_u;
-  uint32_t* done;            // [batch] synthesis arrival tickets (fused finalize)
   int* flag;                 // [batch] item-level fallback flags (AVZ_FALLBACK_BATCH)
   float* pf_gain;            // [batch][nchunk][32][F] IRM gains (AVZ_PF_IRM plans only)
 };
@@ -49,11 +48,10 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
     w->heads = reinterpret_cast<float*>(q); q += sz_ht;
     w->tails = reinterpret_cast<float*>(q); q += sz_ht;
     w->peak_u = reinterpret_cast<uint32_t*>(q); q += sz_b;
-    w->done = reinterpret_cast<uint32_t*>(q); q += sz_b;
     w->flag = reinterpret_cast<int*>(q); q += sz_b;
     w->pf_gain = sz_gain ? reinterpret_cast<float*>(q) : nullptr;
   }
-  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 3 * sz_b + sz_gain;
+  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 2 * sz_b + sz_gain;
 }
 
 struct avz_plan {
@@ -320,7 +318,6 @@ static int prepare_chain(const avz_plan* p, const avz_batch_args* a, int use, av
   k.heads = ws.heads;
   k.tails = ws.tails;
   k.peak_u = ws.peak_u;
-  k.done = ws.done;
   k.flag = ws.flag;
   k.pf_gain = ws.pf_gain;
   if (use == USE_COVARIANCE) {  // that stage produces cov_out only: leave the caller's
@@ -742,7 +739,9 @@ extern "C" long long avz_scene_generate_workspace_bytes(int batch, int n_interfe
   return avz_scene_gen_ws(batch, 1 + n_interferers, n);
 }
 
-constexpr int kMaxInterferers = 254;
+// source s draws Philox stream s (s <= 255 with 255 interferers) and the mic noise draws
+// streams 0x100 + mic, so every stream stays distinct
+constexpr int kMaxInterferers = 255;
 
 extern "C" int avz_scene_generate(int batch, long long start_idx, int n_interferers, int n,
                                   unsigned seed, double mic_d, double c_sound, double fs,
@@ -751,8 +750,8 @@ extern "C" int avz_scene_generate(int batch, long long start_idx, int n_interfer
                                   long long ref_stride, void* workspace,
                                   long long workspace_bytes, void* stream) {
   if (n_interferers < 0 || start_idx < 0) return AVZ_ERR_ARG;
-  // source s draws Philox stream s and mic noise streams 0x100 + mic: at most 255
-  // interferers keep them disjoint; fs >= 4 keeps the 0.25-s envelope block non-empty
+  // at most kMaxInterferers (disjoint Philox streams); fs >= 4 keeps the 0.25-s envelope
+  // block non-empty
   if (n_interferers > kMaxInterferers || !(fs >= 4.0)) return AVZ_ERR_ARG;
   const int n_src = 1 + n_interferers;
   const int rc0 = scene_check(batch, n_src, n, fs, c_sound, mix, mix_stride, ch_stride, tgt, itf,

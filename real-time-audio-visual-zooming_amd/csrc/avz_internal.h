@@ -44,7 +44,6 @@ struct ChainArgs {
   float* heads;               // [B][nchunk][H] chunk's first frame, first-half contribution
   float* tails;               // [B][nchunk][H] chunk's last frame, second-half contribution
   uint32_t* peak_u;           // [B] max |out| over chunk interiors (float bits, atomicMax)
-  uint32_t* done;             // [B] synthesis items finished (fused finalize's arrival ticket)
   float* pf_gain;             // [B][nchunk][32][F] IRM post-filter gain (PF_IRM) or null
   int singular_fallback;      // 0: w = [1, 0]; 1: w = [1/2, 1/2]
   // spectrum-input synthesis (avz_istft): S[b][k][t] complex64 replaces the forward FFT of
@@ -54,10 +53,6 @@ struct ChainArgs {
   long long spec_sb, spec_sf; // complex elements; t stride 1
   int spec_frames;            // frames present in S (frames >= spec_frames read as zero)
   int cov_only;               // solve kernel: write cov_out only (the covariance stage export)
-  // synthesis launch: utterances [syn_b0, syn_b0 + syn_nb) are synthesised and the
-  // finalize items of utterances [fin_b0, fin_b0 + fin_nb) (synthesised by the previous
-  // launch) run in the same grid; the standalone finalize kernel starts at fin_b0
-  int syn_b0, syn_nb, fin_b0, fin_nb;
   int* flag;                  // [B] item-level (batch_mvdr) fallback flags, zeroed per call
   void* const* events;        // host-only: (start, stop) hipEvent_t pairs of the 4 launches, or null
   int n_events;               // host-only: how many of them to use (8, or 2: analysis only)

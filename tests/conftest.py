@@ -56,14 +56,56 @@ def hybrid_bin_causes(Y, M, f, bins, matches, cnt=None):
     b = np.einsum("ft,ft->f", m, Yd[0] * Yd[1].conj()) / nrm
     gap = 2 * np.sqrt((0.5 * (a - e)) ** 2 + np.abs(b) ** 2) / np.maximum(a + e, 1e-300)
     causes = {"mask count": 0, "eigen-gap": 0, "cond branch": 0}
+    assert len(bins) <= MAX_HYBRID_DIFF_BINS, (len(bins), list(bins)[:16])
+    cond = hybrid_cond2(Y, M, f)
     for k in bins:
         if cnt is not None and cnt[k] != m[k].sum():
             causes["mask count"] += 1
         elif gap[k] < 1e-4:
             causes["eigen-gap"] += 1
         else:
+            # a branch decided the other way must sit at the threshold: the oracle's cond_2
+            # within COND_MARGIN (relative) of cond_max, not anywhere
+            margin = abs(cond[k] / O.COND_MAX - 1.0)
+            assert margin <= COND_MARGIN, (k, cond[k], O.COND_MAX)
             alt = [O.hybrid_weights_vec(Y[:, k:k + 1], M[k:k + 1], f[k:k + 1], cond_max=cm)[0]
                    for cm in (1e300, -1.0)]
             assert any(matches(k, w) for w in alt), (k, gap[k])
             causes["cond branch"] += 1
     return causes
+
+
+# differing bins a hybrid comparison may explain at all (0 of 513 on the goldens so far),
+# and how close to cond_max the oracle's cond_2 must be for a branch flip to count
+MAX_HYBRID_DIFF_BINS = 4
+COND_MARGIN = 1e-3
+
+
+def hybrid_cond2(Y, M, f):
+    """The oracle's cond_2 = sigma_max^2 / |det C| of C = [v_tgt, v_int] per bin
+    (Final_pipeline/src/inference.py:72-80), the quantity the hybrid branch compares with
+    cond_max (inf where the reference would take the fallback)."""
+    from oracle import avz_oracle as O
+    Yd = Y.astype(np.complex128)
+    m = (1.0 - M).astype(np.float64)
+    nrm = m.sum(axis=1) + 1e-6
+    a = np.einsum("ft,ft->f", m, np.abs(Yd[0]) ** 2) / nrm
+    e = np.einsum("ft,ft->f", m, np.abs(Yd[1]) ** 2) / nrm
+    b = np.einsum("ft,ft->f", m, Yd[0] * Yd[1].conj()) / nrm
+    lam = 0.5 * (a + e) + np.sqrt((0.5 * (a - e)) ** 2 + np.abs(b) ** 2)
+    u0 = np.where(a >= e, lam - e + 0j, b)
+    u1 = np.where(a >= e, b.conj(), lam - a + 0j)
+    un = np.sqrt(np.abs(u0) ** 2 + np.abs(u1) ** 2)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        u0, u1 = u0 / un, u1 / un
+        a0 = np.abs(u0)
+        v0 = a0 + 1e-10 + 0j
+        v1 = u1 * u0.conj() * (a0 + 1e-10) / a0 ** 2
+        vt = np.stack([O.steering_vector_phase_norm(fk, O.ANGLE_TARGET, O.D_FINAL, O.C_SOUND)[:, 0]
+                       for fk in f])
+        det = vt[:, 0] * v1 - v0 * vt[:, 1]
+        p = np.abs(vt[:, 0]) ** 2 + np.abs(vt[:, 1]) ** 2
+        q = np.abs(v0) ** 2 + np.abs(v1) ** 2
+        r = vt[:, 0].conj() * v0 + vt[:, 1].conj() * v1
+        smax2 = 0.5 * (p + q) + np.sqrt((0.5 * (p - q)) ** 2 + np.abs(r) ** 2)
+        return np.where(np.isfinite(v1) & (np.abs(det) > 0), smax2 / np.abs(det), np.inf)

@@ -52,7 +52,7 @@ def test_strerror_and_host_side_validation():
     # and the 0.25-s envelope block must be non-empty; rejected before any device work
     gen = lambda k, fs: lib.avz_scene_generate(1, 0, k, 16000, 0, 0.01, 343.0, fs, 0.0,  # noqa
                                                30.0, None, 0, 0, None, None, 0, None, 0, None)
-    assert gen(255, 16000.0) == _lib.AVZ_ERR_ARG
+    assert gen(256, 16000.0) == _lib.AVZ_ERR_ARG  # sources 0..255 keep their Philox streams distinct
     assert gen(2, 3.0) == _lib.AVZ_ERR_ARG
     assert gen(2, float("nan")) == _lib.AVZ_ERR_ARG
 

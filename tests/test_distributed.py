@@ -67,3 +67,39 @@ def test_two_rank_gloo_matches_single_process(tmp_path):
     assert [r["SIR_Enh"] for r in single.rows] == [l.split(",")[2] for l in lines[1:]]
     assert single.sums[4] == N_RUNS
     assert single.mean_sir_improvement > 3.0  # the oracle mask really separates the scenes
+
+
+def test_finite_sums_skip_non_finite_rows():
+    """SURVEY 8(e)'s [sums..., n_ok, n]: an utterance with a NaN / inf metric is left out
+    of the sums and of n_ok, the others are summed exactly."""
+    from avz.batch_run import finite_sums
+    a = torch.tensor([1.0, 2.0, float("nan"), 4.0], dtype=torch.float64)
+    b = torch.tensor([10.0, float("-inf"), 30.0, 40.0], dtype=torch.float64)
+    s = finite_sums([a, b], 4).numpy()
+    np.testing.assert_array_equal(s, [5.0, 50.0, 2.0, 4.0])
+    s = finite_sums([a[:2], b[:1].repeat(2)]).numpy()  # no n: [sums, n_ok]
+    np.testing.assert_array_equal(s, [3.0, 20.0, 2.0])
+
+
+def test_batch_run_non_finite_utterance_keeps_row(tmp_path):
+    """One utterance whose enhanced output is all zeros (metrics 0/0): its CSV row is still
+    written (as the reference writes whatever numpy returns), the global sums and n_ok
+    cover the other utterances only."""
+    from avz import batch_run
+
+    def enh(mix, tgt, itf):
+        out = oracle_enhance(mix, tgt, itf)
+        out[1] = 0.0
+        return out
+
+    res = batch_run.run_batch(4, start_idx=3, seconds=SECONDS, batch=4, device="cpu",
+                              enhance=enh, csv_path=str(tmp_path / "m.csv"))
+    ref = batch_run.run_batch(4, start_idx=3, seconds=SECONDS, batch=4, device="cpu",
+                              enhance=oracle_enhance)
+    assert res.sums[4] == 3 and res.sums[5] == 4
+    assert np.all(np.isfinite(res.sums))
+    assert res.rows[1]["SIR_Enh"] in ("nan", "-inf")
+    assert len((tmp_path / "m.csv").read_text().strip().splitlines()) == 5
+    # the three finite utterances sum to the same as the reference run minus utterance 1
+    vals = np.array([[float(r[k]) for k in ("SIR_Base", "SIR_Enh")] for r in ref.rows])
+    np.testing.assert_allclose(res.sums[:2], vals[[0, 2, 3]].sum(0), atol=0.02)

@@ -163,3 +163,28 @@ def test_plan_timing_modes(gpu_device):
     plan.set_timing(False)
     with pytest.raises(AvzError):
         plan.timing()
+
+
+def test_batch_run_gpu_all_zero_utterance_n_ok(gpu_device):
+    """The HIP engine on a batch with one all-zero input: its output and peak are 0, so its
+    deferred-normalised metrics are 0/0 (NaN). n_ok = B - 1, the sums are finite and equal
+    the other utterances' (SURVEY 8(e)'s non-finite guard)."""
+    from avz import batch_run
+    B = 5
+    base = batch_run.gpu_enhancer(max_batch=B, max_samples=16000)
+
+    def enh(mix, tgt, itf):
+        mix = mix.clone()
+        mix[2] = 0.0
+        return base(mix, tgt, itf)
+
+    res = batch_run.run_batch(B, start_idx=20, seconds=1.0, batch=B, device=gpu_device,
+                              enhance=enh)
+    full = batch_run.run_batch(B, start_idx=20, seconds=1.0, batch=B, device=gpu_device)
+    assert res.sums[4] == B - 1 and res.sums[5] == B and full.sums[4] == B
+    assert np.all(np.isfinite(res.sums))
+    assert res.rows[2]["SIR_Enh"] == "nan"
+    keep = [0, 1, 3, 4]
+    sir_b = sum(float(full.rows[j]["SIR_Base"]) for j in keep)
+    sir_e = sum(float(full.rows[j]["SIR_Enh"]) for j in keep)
+    np.testing.assert_allclose(res.sums[:2], [sir_b, sir_e], atol=0.05)

@@ -299,9 +299,9 @@ def test_ipd_identical_channels(avz, gpu_device):
 
 
 def test_multi_round_ragged_batch_equals_single_runs(avz, gpu_device):
-    """A batch larger than one resident synthesis round (128 utterances of 4 chunks at
-    N = 1024 on 256 CUs) with ragged lengths: the round-chained synthesis runs every
-    round's finalize items inside the next round's launch. Every utterance must equal its
+    """A batch larger than one pass of the persistent grids (300 utterances of up to 4
+    chunks: 1200 items over the resident blocks, so each block loops over several items of
+    different utterances and lengths) with ragged lengths. Every utterance must equal its
     own single-utterance run bitwise (same kernels, same per-utterance arithmetic) and the
     peak-normalised output must peak at peak / (peak + eps)."""
     from avz import synth

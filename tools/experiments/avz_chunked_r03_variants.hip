@@ -30,12 +30,56 @@
 
 #include "avz_common.hpp"
 
+#ifndef AVZ_BINS_V1
+#define AVZ_BINS_V1 0
+#endif
+#ifndef AVZ_REFBITS
+#define AVZ_REFBITS 1
+#endif
+
 namespace avz {
 
-// Rejected variants of these kernels (round-chained synthesis, finalize folded into
-// synthesis, the half-size real inverse, precomputed synthesis windows, LDS-twiddle
-// stage-1 stores, ...) are recorded in DESIGN.md §6 and kept under tools/experiments/;
-// this file holds only the shipped paths.
+#ifndef AVZ_SYN_INV2
+#define AVZ_SYN_INV2 1
+#endif
+#ifndef AVZ_SYN_HALF
+#define AVZ_SYN_HALF 0
+#endif
+#ifndef AVZ_SYN_PREWIN
+#define AVZ_SYN_PREWIN 0
+#endif
+// Round-chained synthesis (launch_synth_rounds): off, measured slower
+#ifndef AVZ_SYN_ROUNDS
+#define AVZ_SYN_ROUNDS 0
+#endif
+// The chain's finalize folded into the synthesis kernel: the last chunk item of an
+// utterance to finish (arrival ticket) writes its seams and peak and, for peak
+// normalisation, rescales the utterance in place (fused_finalize).
+// N = 1024 synthesis FFTs with the factored register twiddles (Fft1024x2::stage1_ab_st,
+// stage-1 pairs stored as formed) instead of the block's LDS table: synthesis 73.7-74.1 ->
+// 72.7-73.1 us (profiles/r03d/ab_more.txt r03n2); before the interleaved stores it was neutral
+#ifndef AVZ_SYN_TWAB
+#define AVZ_SYN_TWAB 1
+#endif
+#ifndef AVZ_FUSED_FIN
+#define AVZ_FUSED_FIN 0
+#endif
+
+// 16-B write-through (sc1) buffer stores and L1-bypassing (sc1) loads: the hand-off form of
+// MI355X_MICROARCH's inter-workgroup table (stores all sc1, every storing wave's vmcnt
+// drained before one lane's agent-scope atomic add, the last adder reads with sc1 loads).
+constexpr int kSC1 = 16;  // buffer-op cache policy bit: sc1 (gfx940+)
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st4_sc1(rsrc_t r, int elem, float4 v) {
+  const v4i_t d = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z),
+                   __float_as_int(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(d, r, elem * 4, 0, kSC1);
+}
+__device__ __forceinline__ float4 ld4_sc1(rsrc_t r, int elem) {
+  const v4i_t d = __builtin_amdgcn_raw_buffer_load_b128(r, elem * 4, 0, kSC1);
+  return make_float4(__int_as_float(d.x), __int_as_float(d.y), __int_as_float(d.z),
+                     __int_as_float(d.w));
+}
 
 constexpr int kChunk = 32;      // frames per chunk = bits of one mask word
 constexpr int kCThreads = 256;  // 4 waves
@@ -58,20 +102,14 @@ struct CGeo {
   static_assert(BLOCKS * LDS_BYTES <= 160 * 1024, "resident blocks per CU");
 };
 
-// Synthesis frames per lane group per step: KCfg's SYN_R, except the N = 512 external-mask
-// post-filters, whose strided mask reads need the registers of the second frame (at R = 2
-// they spilled 44-72 B per lane).
-template <int N, int PF>
-constexpr int kSynR = (N == 512 && (PF == PF_EXT_FLOOR || PF == PF_EXT_MUL)) ? 1 : KCfg<N>::SYN_R;
-
-// Synthesis geometry: as CGeo with R frames per lane group per step (NSLOT frame slots,
+// Synthesis geometry: as CGeo with SYN_R frames per lane group per step (NSLOT frame slots,
 // each a lane group's transform area; slot s is "virtual wave" s / FPW of the slot area).
-template <int N, int R_ = KCfg<N>::SYN_R>
+template <int N>
 struct SGeo {
   using C = KCfg<N>;
   static constexpr int NT = kCThreads;
   static constexpr int NWAVE = NT / 64;
-  static constexpr int R = R_;
+  static constexpr int R = C::SYN_R;
   static constexpr int H = N / 2;
   static constexpr int F = N / 2 + 1;
   static constexpr int NSLOT = NWAVE * C::FPW * R;
@@ -118,7 +156,11 @@ struct LaneConst {
   typename KCfg<N>::Fft fft;
   LaneMap<N> lm;
   WinCoef<N> wc;
-  float inv[4];  // synthesis OLA: 1 / window-square sum of samples m0 .. m0 + 3
+  float inv[4];      // synthesis OLA: 1 / window-square sum of samples m0 .. m0 + 3
+  float wi_c, wi_s;  // synthesis, N = 1024: 0.25 cos / sin(2 pi n0 / N), x1 inverse layout
+  // synthesis forward window weights of registers r < PPL/2 (window_apply's w; the upper
+  // half takes 2 a0 - w), formed once instead of per frame
+  float ww[KCfg<N>::PPL / 2];
   __device__ __forceinline__ void init(int tid) {
     const int lane = tid & 63;
     fft.init(lane);
@@ -127,6 +169,21 @@ struct LaneConst {
     const int m0 = 4 * (tid % (N / 8));  // synthesis OLA role (N/2 / 4 float4 groups)
 #pragma unroll
     for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(m0 + i);
+    {
+      using C = KCfg<N>;
+      static_for<0, C::PPL / 2>([&](auto r) {
+        constexpr int j = (C::IN_STRIDE * 32 / N) * r;
+        constexpr float cr = W32::c[j % 32], sr = -W32::s[j % 32];
+        ww[r] = fmaf(wc.as, sr, fmaf(-wc.ac, cr, wc.a0));
+      });
+    }
+    wi_c = wi_s = 0.0f;
+    if constexpr (N == 1024) {
+      double sn, cs;
+      sincospi(2.0 * ((lane & 31) + 512 * (lane >> 5)) / N, &sn, &cs);
+      wi_c = (float)(0.25 * cs);
+      wi_s = (float)(0.25 * sn);
+    }
   }
 };
 
@@ -148,10 +205,27 @@ __device__ __forceinline__ void window_apply(cf (&v)[PPL], float a0, float ac, f
   });
 }
 
-// Window + forward FFT with the lane's twiddles in registers (N = 1024 analysis). Both
-// FFT stages store each output pair as it is formed (the transpose scratch, then the
-// spectrum); after(k) runs right after spectrum output k is stored (the next step's load
-// into register k).
+#ifndef AVZ_IL1
+#define AVZ_IL1 1
+#endif
+#ifndef AVZ_SIL1  // the synthesis kernel's stage-1 stores interleaved too (no gain, off)
+#define AVZ_SIL1 0
+#endif
+#ifndef AVZ_IL_LOADS  // next-step loads issued from inside the FFT's last stage
+#define AVZ_IL_LOADS 1
+#endif
+#ifndef AVZ_REF_ALL  // IBM reference waves store all 32 outputs (loads interleaved for all)
+#define AVZ_REF_ALL 1
+#endif
+#ifndef AVZ_SYN_IL_LOADS  // the same in the synthesis inverse (measured 74.0 -> 75.5 us: off)
+#define AVZ_SYN_IL_LOADS 0
+#endif
+#ifndef AVZ_IL2
+#define AVZ_IL2 1
+#endif
+// Window + forward FFT with the lane's twiddles in registers (N = 1024 analysis).
+// after(k) runs right after spectrum output k is stored (AVZ_IL_LOADS: the next step's
+// load into register k).
 struct NoAfter {
   template <class K>
   __device__ __forceinline__ void operator()(K) const {}
@@ -162,20 +236,36 @@ __device__ __forceinline__ void window_fft_reg(cf (&v)[32], const WinCoef<1024>&
                                                const cf (&tw_reg)[31], const LaneMap<1024>& lm,
                                                After&& after = After{}) {
   window_apply(v, wc.a0, wc.ac, wc.as);
-  fft.stage1_reg_st(v, spec, tw_reg);
-  fft.transpose_read(v, spec);
-  fft.stage2_emit(v, [&](auto k, cf x) {
-    spec[lm.out0 + 32 * k] = x;
-    after(k);
-  });
+#if AVZ_FFT_IL
+  if constexpr (AVZ_IL1) {
+    fft.stage1_reg_st(v, spec, tw_reg);
+    fft.transpose_read(v, spec);
+  } else {
+    fft.stage1_reg(v, tw_reg);
+    fft.transpose(v, spec);
+  }
+  if constexpr (AVZ_IL2) {
+    fft.stage2_emit(v, [&](auto k, cf x) {
+      spec[lm.out0 + 32 * k] = x;
+      after(k);
+    });
+  } else {
+    fft.stage2(v);
+    static_for<0, 32>([&](auto k) { spec[lm.out0 + 32 * k] = v[k]; });
+  }
+#else
+  fft.forward_reg(v, spec, tw_reg);
+  static_for<0, 32>([&](auto k) { spec[lm.out0 + 32 * k] = v[k]; });
+#endif
 }
 
 // Reference pair of the IBM mask (N = 1024, register twiddles): the reference spectrum is
 // only needed for one bit per bin, noise <=> Re(Zr[k] Zr[N - k]) < 0 (ibm_noise). Lane l
-// holds Zr[l + 32 k]; all 32 outputs are stored as formed (so every register takes its
-// next-step load during the stage), then the lane reads back bins l + 32 k, k < 16, with
-// their partners N - (l + 32 k) and publishes their 16 bits as word l of the slot (bytes
-// 0..127). The Nyquist bin (lane 0, k = 16) stays readable at spec[N / 2].
+// holds Zr[l + 32 k]; it stores its upper-half bins (k >= 16) to LDS, reads back the
+// partners N - (l + 32 k) of its lower-half bins (all in the upper half: (32 - l) +
+// 32 (31 - k), or 32 (32 - k) on lane 0; DC pairs with itself) and publishes the 16 bits
+// of bins l + 32 k, k < 16, as word l of the slot (bytes 0..127, below the stored bins).
+// The Nyquist bin (lane 0, k = 16) stays readable at spec[N / 2].
 template <class After = NoAfter>
 __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCoef<1024>& wc,
                                                         const Fft1024x2& fft, cf* spec,
@@ -185,57 +275,125 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
   constexpr int N = 1024;
   window_apply(v, wc.a0, wc.ac, wc.as);
   const int l = lm.out0;
-  fft.stage1_reg_st(v, spec, tw_reg);
-  fft.transpose_read(v, spec);
-  fft.stage2_emit(v, [&](auto k, cf x) {
-    spec[l + 32 * k] = x;
-    after(k);
-  });
+#if AVZ_FFT_IL
+  if constexpr (AVZ_IL1) {
+    fft.stage1_reg_st(v, spec, tw_reg);
+    fft.transpose_read(v, spec);
+  } else {
+    fft.stage1_reg(v, tw_reg);
+    fft.transpose(v, spec);
+  }
+  if constexpr (AVZ_IL2 && AVZ_REF_ALL) {
+    // all 32 outputs stored, so every register takes its next-step load during the stage
+    // (the lower half is read back below instead of being held for the bits)
+    fft.stage2_emit(v, [&](auto k, cf x) {
+      spec[l + 32 * k] = x;
+      after(k);
+    });
+    __builtin_amdgcn_wave_barrier();
+    uint32_t w = 0u;
+    cf zo[16], zp[16];
+    static_for<0, 16>([&](auto k) {
+      const int m = l + 32 * k;
+      zo[k] = spec[m];
+      zp[k] = spec[(N - m) & (N - 1)];
+    });
+    static_for<0, 16>([&](auto k) { w |= (ibm_noise(zo[k], zp[k]) ? 1u : 0u) << k; });
+    reinterpret_cast<uint32_t*>(spec)[l] = w;
+    return;
+  } else if constexpr (AVZ_IL2) {
+    fft.stage2_emit(v, [&](auto k, cf x) {
+      if constexpr (decltype(k)::value >= 16) {
+        spec[l + 32 * k] = x;
+        after(k);
+      }
+    });
+  } else {
+    fft.stage2(v);
+    static_for<16, 32>([&](auto k) { spec[l + 32 * k] = v[k]; });
+  }
+#else
+  fft.forward_reg(v, spec, tw_reg);
+  static_for<16, 32>([&](auto k) { spec[l + 32 * k] = v[k]; });
+#endif
   __builtin_amdgcn_wave_barrier();
   uint32_t w = 0u;
-  cf zo[16], zp[16];
   static_for<0, 16>([&](auto k) {
     const int m = l + 32 * k;
-    zo[k] = spec[m];
-    zp[k] = spec[(N - m) & (N - 1)];
+    cf zp = spec[(N - m) & (N - 1)];
+    if (k == 0 && l == 0) zp = v[0];  // DC: its own partner (index 0 is not stored)
+    w |= (ibm_noise(v[k], zp) ? 1u : 0u) << k;
   });
-  static_for<0, 16>([&](auto k) { w |= (ibm_noise(zo[k], zp[k]) ? 1u : 0u) << k; });
   reinterpret_cast<uint32_t*>(spec)[l] = w;
+  static_for<0, 16>([&](auto k) { after(k); });  // registers 0..15 are free now
 }
 
-// Window + forward FFT of the synthesis kernel and of the N = 512 analysis kernel:
-//  N = 1024: factored register twiddles (Fft1024x2::stage1_ab_st), both stages' outputs
-//            stored as formed (synthesis 73.7-74.1 -> 72.7-73.1 us, profiles/r03d/ab_more.txt);
-//  N = 512, IL512: the interleaved Fft512x2 (the two-block synthesis kernel: 81.0 -> 80.3
-//            us; the three-block N = 512 analysis kernel ran slower with it, 81.3 -> 82.5 us).
-template <int N, bool IL512 = false, class After = NoAfter>
+// window_fft with the lane's window weights precomputed (LaneConst::ww): the synthesis
+// kernel has the registers for them, the analysis kernel does not.
+template <int N>
+__device__ __forceinline__ void window_fft_pre(cf (&v)[KCfg<N>::PPL], const float (&ww)[KCfg<N>::PPL / 2],
+                                               float a0, const typename KCfg<N>::Fft& fft, cf* spec,
+                                               const cf* twid, const LaneMap<N>& lm) {
+  using C = KCfg<N>;
+  const float a2 = a0 + a0;
+  static_for<0, C::PPL / 2>([&](auto r) {
+    v[r] = c_scale(v[r], ww[r]);
+    v[r + C::PPL / 2] = c_scale(v[r + C::PPL / 2], a2 - ww[r]);
+  });
+  fft.forward(v, spec, twid);
+  static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
+}
+
+// IL512: the interleaved Fft512x2 (the synthesis kernel at two blocks per CU: 81.0 -> 80.3
+// us; the three-block N = 512 analysis kernel ran slower with it, 81.3 -> 82.5 us)
+template <int N, bool TWAB = false, bool IL512 = false, class After = NoAfter>
 __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<N>& wc,
                                            const typename KCfg<N>::Fft& fft, cf* spec,
-                                           const LaneMap<N>& lm, After&& after = After{}) {
+                                           const cf* twid, const LaneMap<N>& lm,
+                                           After&& after = After{}) {
   using C = KCfg<N>;
   float a0 = wc.a0, ac = wc.ac, as = wc.as;
   opaque(a0);
   opaque(ac);
   opaque(as);
   window_apply<N>(v, a0, ac, as);
-  if constexpr (N == 1024) {
+  if constexpr (AVZ_FFT_IL && !TWAB && std::is_same<typename C::Fft, Fft1024x2>::value) {
+    if constexpr (AVZ_SIL1) {
+      fft.stage1_lds_st(v, spec, twid);
+      fft.transpose_read(v, spec);
+    } else {
+      fft.stage1(v, twid);
+      fft.transpose(v, spec);
+    }
+    fft.stage2_emit(v, [&](auto k, cf x) { spec[lm.out0 + C::OUT_STRIDE * k] = x; });
+    return;
+  }
+  if constexpr (AVZ_FFT_IL && IL512 && std::is_same<typename C::Fft, Fft512x2>::value) {
+    fft.forward_emit(v, spec, [&](auto k, cf x) {
+      spec[lm.out0 + C::OUT_STRIDE * k] = x;
+      after(k);
+    });
+    return;
+  }
+  if constexpr (AVZ_FFT_IL && TWAB && std::is_same<typename C::Fft, Fft1024x2>::value) {
     fft.stage1_ab_st(v, spec);
     fft.transpose_read(v, spec);
     fft.stage2_emit(v, [&](auto k, cf x) {
       spec[lm.out0 + C::OUT_STRIDE * k] = x;
       after(k);
     });
-  } else if constexpr (IL512) {
-    fft.forward_emit(v, spec, [&](auto k, cf x) {
-      spec[lm.out0 + C::OUT_STRIDE * k] = x;
-      after(k);
-    });
-  } else {
-    fft.forward(v, spec);
-    static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
+    return;
   }
+  if constexpr (TWAB)
+    fft.forward_ab(v, spec);
+  else
+    fft.forward(v, spec, twid);
+  static_for<0, C::PPL>([&](auto k) { spec[lm.out0 + C::OUT_STRIDE * k] = v[k]; });
 }
 
+#ifndef AVZ_SHARE_LOADS
+#define AVZ_SHARE_LOADS 1
+#endif
 // Shared-half loads of a wave's frame pair (Fft1024x2, N = 1024): frames 2w and 2w + 1
 // overlap by N/2 = 16 registers, so the wave loads 1536 samples per stream (24 loads)
 // instead of 2 x 1024 (32). Lane group 1 holds its frame rotated by N/2 — register r < 16
@@ -285,7 +443,13 @@ __device__ __forceinline__ int utt_len(const ChainArgs& A, int b) {
 // pair z = tgt + i int: 2T = zr + conj(zrp), 2I = (zr - conj zrp)/i, and
 // |2T|^2 - |2I|^2 = 4 Re(zr zrp), so noise <=> Re(zr zrp) < 0 (one product, one fma).
 __device__ __forceinline__ bool ibm_noise(cf zr, cf zrp) {
+#if AVZ_BINS_V1
+  const float tr = zr.x + zrp.x, ti = zr.y - zrp.y;
+  const float ir = zr.y + zrp.y, ii = zr.x - zrp.x;
+  return ir * ir + ii * ii > tr * tr + ti * ti;
+#else
   return fmaf(zr.x, zrp.x, -(zr.y * zrp.y)) < 0.0f;
+#endif
 }
 
 // Mask value m and covariance weight of one (bin, frame).
@@ -333,12 +497,15 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   static_assert(kChunk % FB == 0, "steps tile the chunk");
   // IBM without the IRM gains: the reference waves publish per-bin noise bits
   // (window_fft_reg_ibm_bits) instead of the whole reference spectrum
-  constexpr bool REFBITS = N == 1024 && MASK == MASK_IBM && !IRM && !std::is_same<TW, NoTw>::value;
+  constexpr bool REFBITS = AVZ_REFBITS && !AVZ_BINS_V1 && N == 1024 && MASK == MASK_IBM && !IRM &&
+                           !std::is_same<TW, NoTw>::value;
   // shared-half frame-pair loads (pair_loads); needs the twiddle signs of the register path
   // (not IPD: its decisions are pinned bit-exact to the reference's, and the rotated
   // transform's rounding moved one of 1.3e5 on the ipd_test golden)
-  constexpr bool SHARE = N == 1024 && MASK != MASK_IPD && !std::is_same<TW, NoTw>::value;
+  constexpr bool SHARE = AVZ_SHARE_LOADS && N == 1024 && MASK != MASK_IPD &&
+                         !std::is_same<TW, NoTw>::value;
 
+  cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
@@ -349,6 +516,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   if (c >= nch) return;
   if (c == 0 && tid == 0) {
     A.peak_u[b] = 0u;
+    if (A.done) A.done[b] = 0u;  // the synthesis kernel's arrival tickets
     if (A.peak && A.normalize != NORM_PEAK) A.peak[b] = 0.0f;  // finalize's atomicMax target
   }
   const int t0 = c * kChunk;
@@ -401,11 +569,12 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     }
   };
 
-  // IL_LOADS (register-twiddle path): the next step's loads are issued from inside the
+  // AVZ_IL_LOADS (register-twiddle path): the next step's loads are issued from inside the
   // FFT's last stage, register k right after its spectrum output is stored, so their issue
   // overlaps the butterflies; a chunk's last step loads from an empty descriptor (reads 0,
   // no memory traffic). Frames of a next step are >= FB >= 1: no negative sample index.
-  constexpr bool IL_LOADS = N == 1024 && !std::is_same<TW, NoTw>::value;
+  constexpr bool IL_LOADS = AVZ_IL_LOADS && AVZ_FFT_IL && AVZ_IL2 && N == 1024 &&
+                            !std::is_same<TW, NoTw>::value;
   const rsrc_t r_none = make_rsrc(nullptr, 0);
   rsrc_t rn_re = r_none, rn_im = r_none;
   int sp_next = 0;
@@ -481,15 +650,22 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         rn_im = more ? r_im : r_none;
         sp_next = (t0 + (step + 1) * FB + (SHARE ? wave_frame0 : my_frame)) * H - N / 2 + lm.in0;
       }
-      if constexpr (!IL_LOADS) {
-        window_fft<N>(v, wc, fft, my_spec, lm);
-      } else if constexpr (REFBITS) {
+      if constexpr (std::is_same<TW, NoTw>::value) {
+        window_fft<N>(v, wc, fft, my_spec, twid, lm);
+      } else if constexpr (REFBITS && IL_LOADS) {
         if (ref)
           window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm, load_reg);
         else
           window_fft_reg(v, wc, fft, my_spec, tw_reg, lm, load_reg);
-      } else {
+      } else if constexpr (REFBITS) {
+        if (ref)
+          window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm);
+        else
+          window_fft_reg(v, wc, fft, my_spec, tw_reg, lm);
+      } else if constexpr (IL_LOADS) {
         window_fft_reg(v, wc, fft, my_spec, tw_reg, lm, load_reg);
+      } else {
+        window_fft_reg(v, wc, fft, my_spec, tw_reg, lm);
       }
     }
     AVZ_STAMP(3);
@@ -552,7 +728,13 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
               cf x0, x1;
               split_pair2(zm[i], zmp[i], x0, x1);  // 2 y0, 2 y1
               if constexpr (MASK == MASK_IPD) {
-                // the exact angle test of near-colinear bins runs after the loop;
+                // the exact angle test of near-colinear bins runs after the loop
+#if AVZ_BINS_V1
+                const bool clear = ipd_clear(x0, x1) && !((ident_w >> (8 * (g0 + i))) & 1ull);
+                ipd_fix[j] |= (clear ? 0u : 1u) << (g0 + i);
+                const float w = clear ? 1.0f : 0.0f;
+                acc[j].add(x0, x1, w, w);
+#else
                 // ipd_clear on the covariance products themselves: |x0|^2 |x1|^2 and
                 // Im x0 conj(x1) are the test's norm and cross product. Every frame's
                 // products go in at weight 1 (wone: 0 on the DC lane, weighed by the Nyquist
@@ -568,8 +750,10 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
                 acc[j].c11 = fmaf(wone[j], p1, acc[j].c11);
                 acc[j].c01r = fmaf(wone[j], re, acc[j].c01r);
                 acc[j].c01i = fmaf(wone[j], im, acc[j].c01i);
+#endif
                 continue;
               }
+#if !AVZ_BINS_V1
               if constexpr (MASK == MASK_IBM) {
                 bool noise;
                 if constexpr (REFBITS)
@@ -581,6 +765,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
                 if constexpr (IRM) gain[(step * FB + g0 + i) * F + kb] = irm_gain(zr[i], zrp[i]);
                 continue;
               }
+#endif
               bool noise = false;
               float wgt;
               float m;
@@ -618,9 +803,11 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         const int kb = tid + j * NT;
         const int kp = (N - kb) & (N - 1);
         uint32_t f = ipd_fix[j];
+#if !AVZ_BINS_V1
         const bool dc = (j == 0 && tid == 0);
         if (dc) f = 0u;
         ipd_clear_n[j] += dc ? 0 : nvalid - __popc(f);  // weight count: exact integers
+#endif
         while (f) {
           const int i = __builtin_ctz(f);
           f &= f - 1u;
@@ -628,7 +815,11 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
           cf x0, x1;
           split_pair2(Zm[kb], Zm[kp], x0, x1);
           const float w = ((ident_w >> (8 * i)) & 1ull) ? 0.01f : ipd_weight_exact(x0, x1);
+#if AVZ_BINS_V1
+          acc[j].add(x0, x1, w, w);
+#else
           acc[j].add(x0, x1, w - 1.0f, w);  // the products went in at weight 1
+#endif
         }
       }
     }
@@ -643,7 +834,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         float mn = bin_mask<MASK>(A, b, y0, y1, zr, zr, N / 2, f0 + lane, noise, wn);
         if (MASK == MASK_IPD && ((ident_w >> (8 * lane)) & 1ull)) wn = mn = 0.01f;
         an.add(y0, y1, wn, mn);
-        if constexpr (MASK == MASK_IPD) {  // DC of frame `lane`
+        if constexpr (MASK == MASK_IPD && !AVZ_BINS_V1) {  // DC of frame `lane`
           cf d0, d1;
           const cf z0 = Zm[0];
           split_pair2(z0, z0, d0, d1);
@@ -663,14 +854,16 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   // ---- chunk partials
   float* P = A.part + ((long long)b * A.nchunk + c) * 5 * F;
   uint32_t* MW = A.mwords + ((long long)b * A.nchunk + c) * F;
-  constexpr bool DC_NYQ = MASK == MASK_IPD;  // DC sums come from the Nyquist wave
+  constexpr bool DC_NYQ = MASK == MASK_IPD && !AVZ_BINS_V1;  // DC sums come from the Nyquist wave
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
     const int kb = tid + j * NT;
     if (DC_NYQ && kb == 0) continue;
+#if !AVZ_BINS_V1
     // binary weights were folded into the selects: their count is exact in fp32
     if constexpr (MASK == MASK_IBM) acc[j].cm = (float)__popc(bits[j]);
     if constexpr (MASK == MASK_IPD) acc[j].cm += (float)ipd_clear_n[j];
+#endif
     P[0 * F + kb] = acc[j].c00;
     P[1 * F + kb] = acc[j].c11;
     P[2 * F + kb] = acc[j].c01r;
@@ -721,13 +914,16 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysi
   KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
   const int n_items = gx * A.batch;
-  if constexpr (N == 1024) {
+#ifndef AVZ_IPD_TWLDS
+#define AVZ_IPD_TWLDS 0
+#endif
+  if constexpr (N == 1024 && !AVZ_X1 && !(AVZ_IPD_TWLDS && MASK == MASK_IPD)) {
     __syncthreads();
     cf tw_reg[31];
     Fft1024x2 f;
     f.init(threadIdx.x & 63);
     f.load_twiddles(tw_reg, reinterpret_cast<const cf*>(lds + G::TW_OFF));
-    if (MASK != MASK_IPD && (threadIdx.x & 32)) {  // rotated frames: (-1)^k1 (pair_loads)
+    if (AVZ_SHARE_LOADS && MASK != MASK_IPD && (threadIdx.x & 32)) {  // rotated frames: (-1)^k1 (pair_loads)
       static_for<0, 16>([&](auto i) { tw_reg[2 * i] = cf{-tw_reg[2 * i].x, -tw_reg[2 * i].y}; });
     }
     LaneConst<N> K;
@@ -872,12 +1068,17 @@ __global__ void __launch_bounds__(kSrpThreads) avz_srp_kernel(ChainArgs A, SrpAr
 // ================================ synthesis ================================
 // SPEC: the frames' spectra come from A.spec (avz_istft: scipy.signal.istft of a given
 // S[b][k][t]) instead of the forward FFT of the mixture and the apply step.
-template <int N, int PF, bool SPEC>
+template <int N>
+__device__ void fused_finalize(const ChainArgs& A, int b, int T, int nch, float* red);
+template <int N>
+__device__ __forceinline__ void finalize_item(const ChainArgs& A, int c, int b, float* red);
+
+template <int N, int PF, bool SPEC, bool FUSED>
 __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char* lds, int c,
                                                int b, const LaneConst<N>& K) {
   static_assert(!SPEC || PF == PF_NONE, "spectrum input carries its own post-filter");
   using C = KCfg<N>;
-  using G = SGeo<N, kSynR<N, PF>>;
+  using G = SGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
   constexpr int FB = NSLOT;           // frames per step
   constexpr int NPAIR = FB / 2;       // packed inverse FFTs per step
@@ -885,18 +1086,35 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   constexpr int NSG = NT / M4;        // segment groups
   constexpr int SPT = FB / NSG;       // segments per thread per step
   static_assert(SPT * NSG == FB, "OLA mapping");
+  // N = 1024 inverse, one real frame per N/2-point complex transform (HALF): every wave
+  // runs one Fft512x2 pair (frames 2w, 2w + 1 in their own slots), instead of two packed
+  // frames per 1024-point transform on waves 0-1 while waves 2-3 wait at the barrier
+  // (INV2) or four 64-lane x1 transforms. The spectrum input path (SPEC) keeps INV2.
+  constexpr bool HALF = N == 1024 && !AVZ_X1 && AVZ_SYN_HALF && !SPEC;
+  constexpr bool INV2 = N == 1024 && !AVZ_X1 && AVZ_SYN_INV2 && !HALF;
+  constexpr bool TWAB = N == 1024 && !AVZ_X1 && AVZ_SYN_TWAB && !AVZ_SYN_PREWIN;
+  constexpr bool SYN_IL_LOADS = AVZ_SYN_IL_LOADS && AVZ_FFT_IL && INV2 && !TWAB && !SPEC &&
+                                KCfg<N>::SYN_R == 1;
 
+  cf* twid = reinterpret_cast<cf*>(lds + G::TW_OFF);
   float* red = reinterpret_cast<float*>(lds + G::MISC_OFF);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
   const int L = utt_len(A, b);
-  if (L < N) return;  // host validates; a bad device length reports NaN (finalize)
+  if (L < N) {  // host validates; a bad device length reports NaN
+    if (FUSED && c == 0 && tid == 0 && A.peak) A.peak[b] = __builtin_nanf("");
+    return;
+  }
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
   if (c >= nch) return;
   const int t0 = c * kChunk;
   const int nstep = (min(kChunk, T - t0) + FB - 1) / FB;
+  // FUSED: everything the utterance's last item reads back is stored write-through
+  const rsrc_t r_out = make_rsrc(A.out + (long long)b * A.out_stride, (long long)(T - 1) * H);
+  const rsrc_t r_heads = make_rsrc(A.heads + (long long)b * A.nchunk * H, (long long)A.nchunk * H);
+  const rsrc_t r_tails = make_rsrc(A.tails + (long long)b * A.nchunk * H, (long long)A.nchunk * H);
 
   const typename C::Fft fft = K.fft;
   const LaneMap<N> lm = K.lm;
@@ -937,20 +1155,31 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   AVZ_STAMP_INIT();
   if constexpr (!SPEC) issue_loads(0);
 
-  // ---- apply coefficients and post-filter bits of this thread's bins tid + 256 j
+  // ---- apply coefficients and post-filter bits of this thread's bins: tid + 256 j, or
+  // (HALF) the pair tid, N/2 - tid whose spectra meet in bin tid of the N/2-point inverse
   const float4* coef = reinterpret_cast<const float4*>(A.coef) + (long long)b * F;
   const uint32_t* MW = A.mwords + ((long long)b * A.nchunk + c) * F;
+  auto bin_of = [&](int j) { return HALF ? (j == 0 ? tid : H - tid) : tid + j * NT; };
   cf alpha[BPT], beta[BPT];
   uint32_t bits[BPT];
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
-    const float4 cw = SPEC ? make_float4(0.f, 0.f, 0.f, 0.f) : coef[tid + j * NT];
+    const float4 cw = SPEC ? make_float4(0.f, 0.f, 0.f, 0.f) : coef[bin_of(j)];
     alpha[j] = cf{cw.x, cw.y};
     beta[j] = cf{cw.z, cw.w};
-    bits[j] = (PF == PF_IBM_TARGET) ? MW[tid + j * NT] : 0u;
+    bits[j] = (PF == PF_IBM_TARGET) ? MW[bin_of(j)] : 0u;
+  }
+  // HALF: e^{+2 pi i tid / N}, the odd-sample twiddle of the bin pair
+  cf om{1.0f, 0.0f};
+  if constexpr (HALF) {
+    double sn, cs;
+    sincospi(2.0 * tid / N, &sn, &cs);
+    om = cf{(float)cs, (float)sn};
   }
   const bool nyq_wave = (wave == G::NWAVE - 1);
-  cf alpha_n{0, 0}, beta_n{0, 0};  // the Nyquist bin N/2 (outside the pairs)
+  // the one bin outside the pairs: N/2 (Nyquist) or, HALF, N/4 (its own partner)
+  constexpr int KN = HALF ? N / 4 : N / 2;
+  cf alpha_n{0, 0}, beta_n{0, 0};
   uint32_t bits_n = 0u;
   // spectrum input: S[b][k][t] rows (t contiguous); frames past spec_frames read as zero
   const float2* Sb = SPEC ? reinterpret_cast<const float2*>(A.spec) + (long long)b * A.spec_sb
@@ -959,10 +1188,10 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   const bool svec = SPEC && ((A.spec_sb | A.spec_sf) & 1) == 0 &&
                     ((reinterpret_cast<uintptr_t>(A.spec) & 15) == 0);
   if (nyq_wave && !SPEC) {
-    const float4 cw = coef[N / 2];
+    const float4 cw = coef[KN];
     alpha_n = cf{cw.x, cw.y};
     beta_n = cf{cw.z, cw.w};
-    if (PF == PF_IBM_TARGET) bits_n = MW[N / 2];
+    if (PF == PF_IBM_TARGET) bits_n = MW[KN];
   }
   const float* irm = (PF == PF_IRM) ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F
                                     : nullptr;
@@ -994,9 +1223,24 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
   float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);  // previous frame's second half (sgrp 0)
   float* outb = A.out + (long long)b * A.out_stride;
   float peak = 0.0f;
-  const bool ifft_wave = wave < NPAIR / C::FPW;  // waves holding a packed pair
+  const bool ifft_wave = wave < NPAIR / C::FPW;  // waves holding a pair (x2 inverse)
+  float wi_c = 0.f, wi_s = 0.f;  // N = 1024 inverse: 0.25 cos / sin(2 pi n0 / N), x1 layout
+  // HALF: samples 2 m, 2 m + 1 of the Fft512x2 output m = (lane & 15) + 256 h + 16 k
+  float wh_c[2] = {0.f, 0.f}, wh_s[2] = {0.f, 0.f};
+  if constexpr (HALF) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      double sn, cs;
+      sincospi(2.0 * (2 * ((lane & 15) + 256 * ((lane >> 4) & 1)) + e) / N, &sn, &cs);
+      wh_c[e] = (float)(0.25 * cs);
+      wh_s[e] = (float)(0.25 * sn);
+    }
+  } else if constexpr (N == 1024) {
+    wi_c = K.wi_c;
+    wi_s = K.wi_s;
+  }
 
-  lds_barrier();  // the previous item's readers
+  lds_barrier();  // twiddle table
   AVZ_STAMP(4);
   for (int step = 0; step < nstep; ++step) {
     const int f0 = t0 + step * FB;
@@ -1006,15 +1250,28 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     AVZ_STAMP(5);
 #endif
     if constexpr (!SPEC) {
-      window_fft<N, true>(v, wc, fft, my_spec, lm);
+#if AVZ_SYN_PREWIN
+      window_fft_pre<N>(v, K.ww, wc.a0, fft, my_spec, twid, lm);
       if constexpr (G::R > 1) {
 #pragma unroll
         for (int q = 1; q < G::R; ++q)
-          window_fft<N, true>(vq[q - 1], wc, fft, slot_ptr<N>(lds, my_slot + q * RSTRIDE), lm);
+          window_fft_pre<N>(vq[q - 1], K.ww, wc.a0, fft, slot_ptr<N>(lds, my_slot + q * RSTRIDE),
+                            twid, lm);
       }
-      // N = 512: the next step's loads fly through apply, inverse FFT and OLA (the N = 1024
-      // inverse runs in the sample registers, so its loads wait until it is done)
-      if (N != 1024 && more) issue_loads(step + 1);
+#else
+      window_fft<N, TWAB, true>(v, wc, fft, my_spec, twid, lm);
+      if constexpr (G::R > 1) {
+#pragma unroll
+        for (int q = 1; q < G::R; ++q)
+          window_fft<N, TWAB, true>(vq[q - 1], wc, fft, slot_ptr<N>(lds, my_slot + q * RSTRIDE), twid,
+                              lm);
+      }
+#endif
+      // x2 with the x1 inverse: the next step's loads fly through apply, inverse FFT and
+      // OLA. x1 and the two-wave x2 inverse issue them after the inverse FFT, whose
+      // registers they are (measured: issuing them here on the two pairless waves, or
+      // after the overlap-add, costs 1-3 us)
+      if (!AVZ_X1 && !INV2 && more) issue_loads(step + 1);
     }
     lds_barrier();
     AVZ_STAMP(6);
@@ -1038,14 +1295,24 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         zbp[p] = lds_read(Zb + kp);
       }
       // External mask with t-contiguous, 16-B aligned rows (the U-Net / TFLite outputs):
-      // the bin's FB gains of this step in FB/4 16-B loads instead of FB scattered ones,
-      // each loaded for the two pairs that use it (all FB at once held 16 more VGPRs at
-      // N = 512 and spilled 44-72 B)
+      // the bin's FB gains of this step in FB/4 16-B loads instead of FB scattered ones.
       constexpr bool VEC = decltype(vec)::value;
-      const float4* mp = VEC ? reinterpret_cast<const float4*>(
-                                   A.ext_mask + (long long)b * A.mask_sb + (long long)kb * A.mask_sf + f0)
-                             : nullptr;
-      float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      float gv[VEC ? FB : 1];
+      if constexpr (VEC) {
+        const float4* mp = reinterpret_cast<const float4*>(
+            A.ext_mask + (long long)b * A.mask_sb + (long long)kb * A.mask_sf + f0);
+#pragma unroll
+        for (int q = 0; q < FB / 4; ++q) {
+          const float4 m = mp[q];
+          gv[4 * q + 0] = m.x;
+          gv[4 * q + 1] = m.y;
+          gv[4 * q + 2] = m.z;
+          gv[4 * q + 3] = m.w;
+        }
+#pragma unroll
+        for (int i = 0; i < FB; ++i)
+          if constexpr (PF == PF_EXT_FLOOR) gv[i] = fmaxf(gv[i], A.pf_floor);
+      }
 #pragma unroll
       for (int p = 0; p < NPAIR; ++p) {
         const int ta = f0 + 2 * p;
@@ -1053,13 +1320,8 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         const int ia = step * FB + 2 * p;
         float ga, gb;
         if constexpr (VEC) {
-          if (p % 2 == 0) g4 = mp[p / 2];
-          ga = (p % 2 == 0) ? g4.x : g4.z;
-          gb = (p % 2 == 0) ? g4.y : g4.w;
-          if constexpr (PF == PF_EXT_FLOOR) {
-            ga = fmaxf(ga, A.pf_floor);
-            gb = fmaxf(gb, A.pf_floor);
-          }
+          ga = gv[2 * p];
+          gb = gv[2 * p + 1];
         } else {
           ga = gain(bits[j], ia, ta, kb);
           gb = gain(bits[j], ia + 1, ta + 1, kb);
@@ -1071,6 +1333,75 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         Za[kb] = (kb == 0) ? cf{sa.x, sb.x} : cf{sa.x - sb.y, sa.y + sb.x};
       }
     }
+    };
+    // HALF: per frame f (slot f) the spectra S[k], S[N/2 - k] of the thread's pair
+    // k = tid give the N/2-point inverse's input at both (x[n] = sum_k S^[k] e^{2 pi i k n/N}
+    // split into even / odd samples, z[m] = x[2m] + i x[2m+1]):
+    //   Zh[k] = A + i B,  Zh[N/2 - k] = conj(A) + i conj(B),
+    //   A = S[k] + conj(S[N/2 - k]),  B = e^{2 pi i k / N} (S[k] - conj(S[N/2 - k])).
+    // Written in place over the bins just read (no other thread reads them). tid 0 pairs
+    // DC with Nyquist (real parts only, as irfft); its second write lands on bin N/2,
+    // which only it reads and the inverse does not. Bin N/4 (its own partner) is done
+    // below by the Nyquist wave.
+    auto apply_half = [&](auto vec) {
+      constexpr bool VEC = decltype(vec)::value;
+      const int kA = tid, kB = H - tid;
+      float gv[2][VEC ? FB : 1];
+      if constexpr (VEC) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float4* mp = reinterpret_cast<const float4*>(
+              A.ext_mask + (long long)b * A.mask_sb + (long long)bin_of(j) * A.mask_sf + f0);
+#pragma unroll
+          for (int q = 0; q < FB / 4; ++q) {
+            const float4 m = mp[q];
+            gv[j][4 * q + 0] = m.x;
+            gv[j][4 * q + 1] = m.y;
+            gv[j][4 * q + 2] = m.z;
+            gv[j][4 * q + 3] = m.w;
+          }
+#pragma unroll
+          for (int i = 0; i < FB; ++i)
+            if constexpr (PF == PF_EXT_FLOOR) gv[j][i] = fmaxf(gv[j][i], A.pf_floor);
+        }
+      }
+      constexpr int GF = 4;  // frames whose reads are issued together
+#pragma unroll
+      for (int f = 0; f < FB; f += GF) {
+        cf za[GF], zap[GF], zb[GF], zbp[GF];
+#pragma unroll
+        for (int i = 0; i < GF; ++i) {
+          const cf* Z = slot_ptr<N>(lds, f + i);
+          za[i] = lds_read(Z + kA);
+          zap[i] = lds_read(Z + ((N - kA) & (N - 1)));
+          zb[i] = lds_read(Z + kB);
+          zbp[i] = lds_read(Z + (N - kB));
+        }
+#pragma unroll
+        for (int i = 0; i < GF; ++i) {
+          const int t = f0 + f + i, ib = step * FB + f + i;
+          float ga, gb;
+          if constexpr (VEC) {
+            ga = gv[0][f + i];
+            gb = gv[1][f + i];
+          } else {
+            ga = gain(bits[0], ib, t, kA);
+            gb = gain(bits[1], ib, t, kB);
+          }
+          cf sa = apply_bin(alpha[0], beta[0], za[i], zap[i], ga);
+          cf sb = apply_bin(alpha[1], beta[1], zb[i], zbp[i], gb);
+          if (tid == 0) {  // DC and Nyquist: irfft keeps the real parts
+            sa.y = 0.0f;
+            sb.y = 0.0f;
+          }
+          const cf a = {sa.x + sb.x, sa.y - sb.y};  // S[k] + conj S[N/2 - k]
+          const cf d = {sa.x - sb.x, sa.y + sb.y};  // S[k] - conj S[N/2 - k]
+          const cf bb = c_mul(om, d);
+          cf* Z = slot_ptr<N>(lds, f + i);
+          Z[kA] = {a.x - bb.y, a.y + bb.x};
+          Z[kB] = {a.x + bb.y, bb.x - a.y};
+        }
+      }
     };
     // spectrum input: the step's frames of the thread's bins straight from S, packed as
     // above (16-B row segments when the rows are aligned and the step is complete)
@@ -1109,6 +1440,11 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         spec_phase(std::true_type{});
       else
         spec_phase(std::false_type{});
+    } else if constexpr (HALF) {
+      if ((PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) && mask_vec && f0 + FB <= T)  // block-uniform
+        apply_half(std::true_type{});
+      else
+        apply_half(std::false_type{});
     } else if constexpr (PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) {
       if (mask_vec && f0 + FB <= T)  // wave-uniform
         apply_phase(std::true_type{});
@@ -1125,7 +1461,14 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         slot_ptr<N>(lds, 2 * lane)[N / 2] = {xa, xb};
       }
     }
-    if (!SPEC && nyq_wave && lane < NPAIR) {  // Nyquist bin: frame pair `lane`
+    if (HALF && nyq_wave && lane < FB) {  // bin N/4 of frame `lane`: Zh = 2 conj(S)
+      const int t = f0 + lane;
+      cf* Z = slot_ptr<N>(lds, lane);
+      const float g = gain(bits_n, step * FB + lane, t, N / 4);
+      const cf s = apply_bin(alpha_n, beta_n, Z[N / 4], Z[3 * N / 4], g);
+      Z[N / 4] = {2.0f * s.x, -2.0f * s.y};
+    }
+    if (!HALF && !SPEC && nyq_wave && lane < NPAIR) {  // Nyquist bin: frame pair `lane`
       const int ta = f0 + 2 * lane;
       if (ta < T) {
         const int ia = step * FB + 2 * lane;
@@ -1140,46 +1483,134 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     lds_barrier();
     AVZ_STAMP(7);
 
-    // ---- inverse FFT of the packed pairs -> windowed frame contributions in slot 2p+1:
-    // one packed pair per lane group, two transforms per wave on the waves holding pairs.
-    // The N = 1024 transform runs in the sample registers v (the round-1 x1 form with four
-    // waves and the loads in flight ran 77.5 vs 73.6 us), so the next step's loads are
-    // issued after it (issuing them on the pairless waves first, inside the inverse, or
-    // after the overlap-add measured 1-3 us slower).
-    if (ifft_wave) {
+    // ---- inverse FFT of the packed pairs -> windowed frame contributions in slot 2p+1
+    //      (HALF: of each frame's N/2-point input -> its own slot)
+    if constexpr (HALF) {
+      cf u[16];
+      cf* Zi = slot_ptr<N>(lds, my_slot);
+      static_for<0, 16>([&](auto r) { u[r] = c_conj(lds_read(Zi + (lane & 31) + 32 * r)); });
+      Fft512x2::forward_tw1024(u, Zi + H, twid, lane);
+      // u[k] = conj(z[m]), m = (lane & 15) + 16 k + 256 h: samples 2m (Re z), 2m + 1 (Im z)
+      float2* Cp = reinterpret_cast<float2*>(Zi);
+      const int mh = (lane & 15) + 256 * ((lane >> 4) & 1);
+      static_for<0, 16>([&](auto k) {
+        constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi (32 k) / N
+        const float we = fmaf(wh_s[0], sk, fmaf(-wh_c[0], ck, 0.25f));
+        const float wo = fmaf(wh_s[1], sk, fmaf(-wh_c[1], ck, 0.25f));
+        Cp[mh + 16 * k] = make_float2(u[k].x * we, -u[k].y * wo);
+      });
+    } else if constexpr (N == 1024 && AVZ_X1) {
+      // two pairs: waves 0-1 run one 64-lane 1024-point transform each (register twiddles;
+      // output register k of lane (l, h) is sample l + 512 h + 32 k)
+      if (wave < NPAIR) {
+        cf u[16];
+        cf* Zi = slot_ptr<N>(lds, 2 * wave);
+        static_for<0, 16>([&](auto r) { u[r] = c_conj(Zi[64 * r + lane]); });
+        fft.forward(u, Zi, twid);
+        float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * wave + 1));
+        const int n0 = (lane & 31) + 512 * (lane >> 5);
+        float ws = wi_s, wcs = wi_c;
+        opaque(ws);
+        opaque(wcs);
+        static_for<0, 16>([&](auto k) {
+          constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+          const float w = fmaf(ws, sk, fmaf(-wcs, ck, 0.25f));
+          const int n = n0 + 32 * k;
+          Cp[n] = u[k].x * w;       // frame 2p   (real part of the inverse)
+          Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
+        });
+      }
+    } else if constexpr (N == 1024 && !INV2) {
+      // four pairs, four waves: one 64-lane 1024-point transform each (x1 layout:
+      // output register k of lane (l, h) is sample l + 512 h + 32 k)
+      cf u[16];
+      cf* Zi = slot_ptr<N>(lds, 2 * wave);
+      static_for<0, 16>([&](auto r) { u[r] = c_conj(lds_read(Zi + 64 * r + lane)); });
+      Fft1024::forward_tw(u, Zi, twid, lane);
+      float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * wave + 1));
+      const int n0 = (lane & 31) + 512 * (lane >> 5);
+      static_for<0, 16>([&](auto k) {
+        constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+        const float w = fmaf(wi_s, sk, fmaf(-wi_c, ck, 0.25f));
+        const int n = n0 + 32 * k;
+        Cp[n] = u[k].x * w;       // frame 2p   (real part of the inverse)
+        Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
+      });
+    } else if (ifft_wave) {
+      // N = 512, and N = 1024 with AVZ_SYN_INV2: one packed pair per lane group, two
+      // transforms per wave on the waves holding pairs (the 1024-point x2 form runs in the
+      // sample registers v, so the next step's loads wait until it is done)
       const int p = wave * C::FPW + lm.grp;
       cf* Zi = slot_ptr<N>(lds, 2 * p);
       auto inverse = [&](cf (&u)[PPL]) {
         static_for<0, PPL>([&](auto r) { u[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
         float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
-        auto emit = [&](auto k, cf x) {
+        if constexpr (AVZ_FFT_IL && N == 1024) {
+          if constexpr (TWAB) {
+            fft.stage1_ab_st(u, Zi);
+            fft.transpose_read(u, Zi);
+          } else if constexpr (AVZ_SIL1) {
+            fft.stage1_lds_st(u, Zi, twid);
+            fft.transpose_read(u, Zi);
+          } else {
+            fft.stage1(u, twid);
+            fft.transpose(u, Zi);
+          }
+          // INV2 runs in the sample registers: the next step's load into register k is
+          // issued as soon as output k is stored (SYN_IL_LOADS; an empty descriptor after
+          // the chunk's last step)
+          const rsrc_t rz = make_rsrc(nullptr, 0);
+          const rsrc_t rn0 = more ? r_m0 : rz, rn1 = more ? r_m1 : rz;
+          const int s0n = (t0 + (step + 1) * FB + my_slot) * H - N / 2 + lm.in0;
+          fft.stage2_emit(u, [&](auto k, cf x) {
+            constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+            const float w = fmaf(wc.ss, sk, fmaf(-wc.sc, ck, wc.s0));
+            const int n = lm.out0 + C::OUT_STRIDE * k;
+            Cp[n] = x.x * w;       // frame 2p   (real part of the inverse)
+            Cp[N + n] = -x.y * w;  // frame 2p+1 (imaginary part; conjugation trick)
+            if constexpr (SYN_IL_LOADS) {
+              u[k].x = bload_nn(rn0, s0n + C::IN_STRIDE * k);
+              u[k].y = bload_nn(rn1, s0n + C::IN_STRIDE * k);
+            }
+          });
+          return;
+        }
+        if constexpr (AVZ_FFT_IL && N == 512) {
+          fft.forward_emit(u, Zi, [&](auto k, cf x) {
+            constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+            const float w = fmaf(wc.ss, sk, fmaf(-wc.sc, ck, wc.s0));
+            const int n = lm.out0 + C::OUT_STRIDE * k;
+            Cp[n] = x.x * w;       // frame 2p   (real part of the inverse)
+            Cp[N + n] = -x.y * w;  // frame 2p+1 (imaginary part; conjugation trick)
+          });
+          return;
+        }
+        if constexpr (TWAB)
+          fft.forward_ab(u, Zi);
+        else
+          fft.forward(u, Zi, twid);
+        static_for<0, PPL>([&](auto k) {
           constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
           const float w = fmaf(wc.ss, sk, fmaf(-wc.sc, ck, wc.s0));
           const int n = lm.out0 + C::OUT_STRIDE * k;
-          Cp[n] = x.x * w;       // frame 2p   (real part of the inverse)
-          Cp[N + n] = -x.y * w;  // frame 2p+1 (imaginary part; conjugation trick)
-        };
-        if constexpr (N == 1024) {
-          fft.stage1_ab_st(u, Zi);
-          fft.transpose_read(u, Zi);
-          fft.stage2_emit(u, emit);
-        } else {
-          fft.forward_emit(u, Zi, emit);
-        }
+          Cp[n] = u[k].x * w;       // frame 2p   (real part of the inverse)
+          Cp[N + n] = -u[k].y * w;  // frame 2p+1 (imaginary part; conjugation trick)
+        });
       };
-      if constexpr (N == 1024) {
+      if constexpr (INV2) {
         inverse(v);
       } else {
         cf u[PPL];
         inverse(u);
       }
     }
-    if (N == 1024 && !SPEC && more) issue_loads(step + 1);
+    if ((AVZ_X1 || INV2) && !SPEC && more && !(SYN_IL_LOADS && ifft_wave)) issue_loads(step + 1);
     lds_barrier();
     AVZ_STAMP(8);
 
     // ---- overlap-add: segment j = f0 - 1 + s = frame s-1 (2nd half) + frame s (1st half)
     auto cframe = [&](int f) -> const float* {
+      if constexpr (HALF) return reinterpret_cast<const float*>(slot_ptr<N>(lds, f));
       return reinterpret_cast<const float*>(slot_ptr<N>(lds, 2 * (f >> 1) + 1)) + (f & 1) * N;
     };
 #pragma unroll
@@ -1187,7 +1618,10 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       const int s = sgrp + si * NSG;
       const float4 vb = *reinterpret_cast<const float4*>(cframe(s) + m0);
       if (s == 0 && step == 0) {  // chunk's first frame: finalize adds the previous tail
-        *reinterpret_cast<float4*>(A.heads + ((long long)b * A.nchunk + c) * H + m0) = vb;
+        if constexpr (FUSED)
+          st4_sc1(r_heads, c * H + m0, vb);
+        else
+          *reinterpret_cast<float4*>(A.heads + ((long long)b * A.nchunk + c) * H + m0) = vb;
         continue;
       }
       const int j = f0 - 1 + s;
@@ -1199,7 +1633,10 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
         o.y = (va.y + vb.y) * inv[1];
         o.z = (va.z + vb.z) * inv[2];
         o.w = (va.w + vb.w) * inv[3];
-        *reinterpret_cast<float4*>(outb + (long long)j * H + m0) = o;
+        if constexpr (FUSED)
+          st4_sc1(r_out, j * H + m0, o);
+        else
+          *reinterpret_cast<float4*>(outb + (long long)j * H + m0) = o;
         peak = fmaxf(peak, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
       }
     }
@@ -1207,32 +1644,137 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
     lds_barrier();
     AVZ_STAMP(9);
   }
-  if (sgrp == 0 && nstep * FB == kChunk)  // full chunk: its last frame's tail
-    *reinterpret_cast<float4*>(A.tails + ((long long)b * A.nchunk + c) * H + m0) = carry;
+  if (sgrp == 0 && nstep * FB == kChunk) {  // full chunk: its last frame's tail
+    if constexpr (FUSED)
+      st4_sc1(r_tails, c * H + m0, carry);
+    else
+      *reinterpret_cast<float4*>(A.tails + ((long long)b * A.nchunk + c) * H + m0) = carry;
+  }
 
   // ---- block max |out| -> utterance running max (non-negative floats order as uints)
   for (int o = 32; o > 0; o >>= 1) peak = fmaxf(peak, __shfl_xor(peak, o, 64));
   if (lane == 0) red[wave] = peak;
+  if constexpr (FUSED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores
   __syncthreads();
   if (tid == 0) {
     float pk = red[0];
 #pragma unroll
     for (int w = 1; w < G::NWAVE; ++w) pk = fmaxf(pk, red[w]);
     atomicMax(A.peak_u + b, __float_as_uint(pk));
+    if constexpr (FUSED) {  // arrival ticket, behind the block's drained stores and its max
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t t = atomicAdd(A.done + b, 1u);
+      reinterpret_cast<int*>(red)[G::NWAVE] = (t + 1u == (uint32_t)nch) ? 1 : 0;
+    }
+  }
+  if constexpr (FUSED) {
+    __syncthreads();
+    if (reinterpret_cast<const int*>(red)[G::NWAVE]) fused_finalize<N>(A, b, T, nch, red);
+    __syncthreads();
   }
   AVZ_STAMP(10);
 }
 
 // Persistent grid over (chunk, utterance) items, as avz_analysis_kernel.
-template <int N, int PF, bool SPEC = false>
+template <int N, int PF, bool SPEC = false, bool FUSED = false>
 __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_synthesis_kernel(ChainArgs A) {
+  using G = SGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
+  KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
   LaneConst<N> K;
   K.init(threadIdx.x);
-  const int nsyn = gx * A.batch;
-  for (int it = blockIdx.x; it < nsyn; it += gridDim.x)
-    synthesis_item<N, PF, SPEC>(A, lds, it % gx, it / gx, K);
+  // finalize items of the previous launch's utterances, run by the upper half of the grid
+  // before its synthesis items and by the lower half after them, so the resident blocks of
+  // a CU (dispatched a grid half apart) mostly pair an HBM-bound finalize item with a
+  // compute-bound synthesis item
+  const int nsyn = gx * A.syn_nb;
+  if constexpr (AVZ_SYN_ROUNDS) {  // compiled out otherwise: the finalize item costs registers
+    float* red = reinterpret_cast<float*>(lds + G::MISC_OFF);
+    constexpr int FCH = N >= 1024 ? 1 : 1024 / N;  // kFinChunks<N> (defined with finalize)
+    const int fg = (gx + FCH - 1) / FCH;
+    const int nfin = fg * A.fin_nb;
+    auto fin_items = [&]() {
+      for (int it = blockIdx.x; it < nfin; it += gridDim.x) {
+        __syncthreads();  // red[] of the previous item
+        finalize_item<N>(A, it % fg, A.fin_b0 + it / fg, red);
+      }
+    };
+    const bool fin_first = blockIdx.x >= gridDim.x / 2;
+    if (fin_first) fin_items();
+    for (int it = blockIdx.x; it < nsyn; it += gridDim.x) {
+      if (nfin > 0) __syncthreads();
+      synthesis_item<N, PF, SPEC, FUSED>(A, lds, it % gx, A.syn_b0 + it / gx, K);
+    }
+    if (!fin_first) fin_items();
+  } else {
+    for (int it = blockIdx.x; it < nsyn; it += gridDim.x)
+      synthesis_item<N, PF, SPEC, FUSED>(A, lds, it % gx, A.syn_b0 + it / gx, K);
+  }
+}
+
+// Finalize of utterance b inside the synthesis kernel, run by the block whose item was the
+// utterance's last to arrive (every other item's interior, head and tail stores are
+// write-through and drained before its ticket): seams 32 cc - 1 = tails[cc - 1] + heads[cc]
+// (cc = 1 .. nch - 1), the utterance peak (interiors' atomicMax and the seams), peak[b];
+// NORM_PEAK also rescales every interior segment in place (L1-bypassing loads). The same
+// arithmetic as avz_finalize_kernel.
+template <int N>
+__device__ void fused_finalize(const ChainArgs& A, int b, int T, int nch, float* red) {
+  constexpr int NT = kCThreads, H = N / 2, H4 = H / 4, NWAVE = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* outb = A.out + (long long)b * A.out_stride;
+  const rsrc_t r_h = make_rsrc(A.heads + (long long)b * A.nchunk * H, (long long)A.nchunk * H);
+  const rsrc_t r_t = make_rsrc(A.tails + (long long)b * A.nchunk * H, (long long)A.nchunk * H);
+  const rsrc_t r_o = make_rsrc(outb, (long long)(T - 1) * H);
+  const int nseam4 = (nch - 1) * H4;
+  auto seam4 = [&](int idx) -> float4 {  // float4 group idx of the seams, in segment order
+    const int cc = idx / H4 + 1, m = 4 * (idx % H4);
+    const float4 t = ld4_sc1(r_t, (cc - 1) * H + m);
+    const float4 h = ld4_sc1(r_h, cc * H + m);
+    return make_float4((t.x + h.x) * inv_wsum<N>(m), (t.y + h.y) * inv_wsum<N>(m + 1),
+                       (t.z + h.z) * inv_wsum<N>(m + 2), (t.w + h.w) * inv_wsum<N>(m + 3));
+  };
+  float pk = 0.0f;
+  for (int idx = tid; idx < nseam4; idx += NT) {
+    const float4 x = seam4(idx);
+    pk = fmaxf(pk, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+  }
+  for (int o = 32; o > 0; o >>= 1) pk = fmaxf(pk, __shfl_xor(pk, o, 64));
+  if (lane == 0) red[wave] = pk;
+  __syncthreads();
+  pk = __uint_as_float(__hip_atomic_load(A.peak_u + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+  for (int w = 0; w < NWAVE; ++w) pk = fmaxf(pk, red[w]);
+  if (tid == 0 && A.peak) A.peak[b] = pk;
+  const bool norm = A.normalize == NORM_PEAK;
+  const float scale = norm ? 1.0f / (pk + A.norm_eps) : 1.0f;
+  for (int idx = tid; idx < nseam4; idx += NT) {
+    float4 x = seam4(idx);
+    x.x *= scale; x.y *= scale; x.z *= scale; x.w *= scale;
+    const int cc = idx / H4 + 1, m = 4 * (idx % H4);
+    *reinterpret_cast<float4*>(outb + (long long)(kChunk * cc - 1) * H + m) = x;
+  }
+  if (!norm) return;
+  // interior segments j < T - 1, j % 32 != 31 (the seams, written above): 16 loads in
+  // flight per lane, issued unconditionally (the descriptor returns 0 past the end; seam
+  // positions are loaded and dropped) so they are not serialised behind branches
+  constexpr int U = 16;
+  const int n4 = (T - 1) * H4;
+  float4* o4 = reinterpret_cast<float4*>(outb);
+  for (int base = 0; base < n4; base += U * NT) {
+    float4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = ld4_sc1(r_o, 4 * (base + u * NT + tid));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * NT + tid;
+      if (i < n4 && (i / H4) % kChunk != kChunk - 1) {
+        x[u].x *= scale; x[u].y *= scale; x[u].z *= scale; x[u].w *= scale;
+        o4[i] = x[u];
+      }
+    }
+  }
 }
 
 // ================================ finalize ================================
@@ -1345,7 +1887,7 @@ __device__ __forceinline__ void finalize_item(const ChainArgs& A, int q, int b, 
 template <int N>
 __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
   __shared__ float red[kCThreads / 64];
-  finalize_item<N>(A, blockIdx.x, blockIdx.y, red);
+  finalize_item<N>(A, blockIdx.x, A.fin_b0 + blockIdx.y, red);
 }
 
 // Grid x of the finalize kernel: FCH-chunk groups of the longest utterance.
@@ -1361,16 +1903,48 @@ extern "C" int avz_chunk_frames(void) { return kChunk; }
 static int resident_cus();
 
 // The synthesis launch of the chain and of the stage exports (persistent grid).
-template <int N, int PF, bool SPEC = false>
+// One synthesis launch over utterances [a->syn_b0, + syn_nb) with the finalize items of
+// [fin_b0, + fin_nb) in the same persistent grid.
+template <int N, int PF, bool FUSED = false>
 static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
-  constexpr int lds = SGeo<N, kSynR<N, PF>>::LDS_BYTES;
-  if (!lds_ready<avz_synthesis_kernel<N, PF, SPEC>>(lds)) return -3;
-  const int n_items = nch * a->batch;
+  constexpr int lds = SGeo<N>::LDS_BYTES;
+  if (!lds_ready<avz_synthesis_kernel<N, PF, false, FUSED>>(lds)) return -3;
+  const int n_items = nch * std::max(a->syn_nb, a->fin_nb);
   if (n_items == 0) return 0;
   const dim3 sgrid((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus()));
-  hipExtLaunchKernelGGL((avz_synthesis_kernel<N, PF, SPEC>), sgrid, dim3(kCThreads), lds, st, e0,
-                        e1, 0, *a);
+  hipExtLaunchKernelGGL((avz_synthesis_kernel<N, PF, false, FUSED>), sgrid, dim3(kCThreads), lds,
+                        st, e0, e1, 0, *a);
+  return 0;
+}
+
+// The chain's synthesis + finalize (non-fused): the batch is synthesised in rounds of as
+// many utterances as the resident grid holds; every round's launch also runs the previous
+// round's finalize items, so that HBM-bound pass overlaps compute-bound synthesis, and only
+// the last round's finalize runs as its own kernel. One round (or AVZ_SYN_ROUNDS 0): one
+// synthesis launch and one finalize launch.
+template <int N, int PF>
+static int launch_synth_rounds(const ChainArgs* a, hipStream_t st, hipEvent_t e4, hipEvent_t e5,
+                               hipEvent_t e6, hipEvent_t e7) {
+  const int nch = (a->max_frames + kChunk - 1) / kChunk;
+  const int slots = KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus();
+  const int per_round = AVZ_SYN_ROUNDS ? std::max(1, slots / nch) : a->batch;
+  ChainArgs s = *a;
+  int prev_b0 = 0, prev_nb = 0;
+  for (int b0 = 0; b0 < a->batch; b0 += per_round) {
+    s.syn_b0 = b0;
+    s.syn_nb = std::min(per_round, a->batch - b0);
+    s.fin_b0 = prev_b0;
+    s.fin_nb = prev_nb;
+    const bool first = b0 == 0, last = b0 + per_round >= a->batch;
+    if (launch_synthesis<N, PF>(&s, st, first ? e4 : nullptr, last ? e5 : nullptr) != 0) return -3;
+    prev_b0 = s.syn_b0;
+    prev_nb = s.syn_nb;
+  }
+  ChainArgs f = *a;
+  f.fin_b0 = prev_b0;
+  hipExtLaunchKernelGGL(avz_finalize_kernel<N>, dim3(fin_groups<N>(nch), prev_nb), dim3(kCThreads), 0, st, e6,
+                        e7, 0, f);
   return 0;
 }
 
@@ -1402,6 +1976,7 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   if (!lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM>>(lds)) return -3;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
+  const dim3 grid(nch, a->batch);
   const int n_items = nch * a->batch;
   const dim3 pgrid((unsigned)std::min(n_items, CGeo<N>::BLOCKS * resident_cus()));
   constexpr int F = N / 2 + 1;
@@ -1421,9 +1996,22 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   } else {
     hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), evt(3), 0, *a);
   }
-  if (launch_synthesis<N, PF>(a, st, evt(4), evt(5)) != 0) return -3;
-  hipExtLaunchKernelGGL(k3, dim3(fin_groups<N>(nch), a->batch), dim3(kCThreads), 0, st, evt(6),
-                        evt(7), 0, *a);
+#if AVZ_FUSED_FIN
+  (void)k3;
+  (void)grid;
+  ChainArgs af = *a;
+  af.syn_b0 = 0;
+  af.syn_nb = a->batch;
+  af.fin_nb = 0;
+  if (launch_synthesis<N, PF, true>(&af, st, evt(4), evt(5)) != 0) return -3;
+  if (evt(6) && (hipEventRecord(evt(6), st) != hipSuccess ||  // finalize: fused (0 ms)
+                 hipEventRecord(evt(7), st) != hipSuccess))
+    return -3;
+#else
+  (void)k3;
+  (void)grid;
+  if (launch_synth_rounds<N, PF>(a, st, evt(4), evt(5), evt(6), evt(7)) != 0) return -3;
+#endif
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -1531,17 +2119,30 @@ extern "C" int avz_launch_covariance(int n_fft, int mask_mode, const ChainArgs* 
 
 template <int N, int PF, bool SPEC>
 static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
+  constexpr int lds = SGeo<N>::LDS_BYTES;
+  if (SPEC && !lds_ready<avz_synthesis_kernel<N, PF, SPEC>>(lds)) return -3;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
+  const int n_items = nch * a->batch;
   // no analysis pass in these stages: it is the analysis kernel that resets peak_u
   if (hipMemsetAsync(a->peak_u, 0, sizeof(uint32_t) * a->batch, st) != hipSuccess) return -3;
   if (a->peak && a->normalize != NORM_PEAK &&
       hipMemsetAsync(a->peak, 0, sizeof(float) * a->batch, st) != hipSuccess)
     return -3;
-  // one synthesis launch over the batch, then the finalize kernel
-  if (launch_synthesis<N, PF, SPEC>(a, st, nullptr, nullptr) != 0) return -3;
+  ChainArgs s = *a;  // one synthesis launch over the batch, then the finalize kernel
+  s.syn_b0 = 0;
+  s.syn_nb = a->batch;
+  s.fin_b0 = 0;
+  s.fin_nb = 0;
+  if constexpr (SPEC) {
+    hipLaunchKernelGGL((avz_synthesis_kernel<N, PF, SPEC>),
+                       dim3((unsigned)std::min(n_items, KCfg<N>::SYN_BLOCKS_PER_CU * resident_cus())),
+                       dim3(kCThreads), lds, st, s);
+  } else {
+    if (launch_synthesis<N, PF>(&s, st, nullptr, nullptr) != 0) return -3;
+  }
   hipLaunchKernelGGL(avz_finalize_kernel<N>, dim3(fin_groups<N>(nch), a->batch), dim3(kCThreads), 0,
-                     st, *a);
+                     st, s);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -68,8 +68,35 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// AVZ_X1: the N = 1024 chain kernels run one 1024-point FFT per wave (Fft1024, 16 points
+// per lane, one 8.4 KB LDS slot per wave) instead of two per wave (Fft1024x2, 32 points
+// per lane, two slots): a quarter of the LDS and about half the VGPRs per wave, so four
+// 4-wave blocks fit a CU (four waves per SIMD instead of two).
+#ifndef AVZ_X1
+#define AVZ_X1 0
+#endif
+
 template <int N>
 struct KCfg;
+#if AVZ_X1
+template <>
+struct KCfg<1024> {
+  using Fft = Fft1024;
+  static constexpr int PPL = Fft::PPL;       // 16 complex points per lane
+  static constexpr int FPW = 1;              // one FFT per wave
+  static constexpr int GROUP_BYTES = 32 * 33 * 8;
+  static constexpr int WAVE_BYTES = GROUP_BYTES;
+  static constexpr int IN_STRIDE = 64;       // lane L, reg r <-> x[64 r + L]
+  static constexpr int OUT_STRIDE = 32;      // lane (k1, h), reg k <-> X[k1 + 32 k + 512 h]
+  static constexpr int TW_BYTES = Fft1024::TW_ENTRIES * 8;  // P, Q table (3 KB)
+  static constexpr int BLOCKS_PER_CU = 4;
+#ifdef AVZ_SYN_BLOCKS
+  static constexpr int SYN_BLOCKS_PER_CU = AVZ_SYN_BLOCKS;
+#else
+  static constexpr int SYN_BLOCKS_PER_CU = 4;
+#endif
+};
+#else
 template <>
 struct KCfg<1024> {
   using Fft = Fft1024x2;
@@ -84,6 +111,7 @@ struct KCfg<1024> {
   static constexpr int SYN_BLOCKS_PER_CU = 2;
   static constexpr int SYN_R = 1;  // synthesis frames per lane group per step
 };
+#endif
 template <>
 struct KCfg<512> {
   using Fft = Fft512x2;
@@ -94,14 +122,26 @@ struct KCfg<512> {
   static constexpr int IN_STRIDE = 32;
   static constexpr int OUT_STRIDE = 16;
   static constexpr int TW_BYTES = 0;
+#ifdef AVZ_B512
+  static constexpr int BLOCKS_PER_CU = AVZ_B512;
+#else
   // analysis at 3 blocks (12 waves) per CU: 168 VGPRs, 3 x 35 KB LDS; 97.9 -> 81.0 us at
   // B = 256 (profiles/r03/n512_occupancy.txt); 4 spills and runs 85 us, the synthesis
   // gains nothing from 3 (spills at 168 VGPRs)
   static constexpr int BLOCKS_PER_CU = 3;
+#endif
+#ifdef AVZ_SB512
+  static constexpr int SYN_BLOCKS_PER_CU = AVZ_SB512;
+#else
   static constexpr int SYN_BLOCKS_PER_CU = 2;
+#endif
   // synthesis frames per lane group per step: 2 -> 16 frames (and 8 packed inverse pairs,
   // two per wave) per step in the same 70 KB of LDS as N = 1024's 8
+#ifdef AVZ_SYN_R512
+  static constexpr int SYN_R = AVZ_SYN_R512;
+#else
   static constexpr int SYN_R = 2;
+#endif
 };
 
 template <int N, int NT>
@@ -136,7 +176,11 @@ struct LaneMap {
   int grp;    // lane group (N=512: which of the two FFTs; N=1024: 0)
   int out0;   // output index of register 0
   __device__ __forceinline__ void init(int lane) {
-    if constexpr (N == 1024) {
+    if constexpr (N == 1024 && AVZ_X1) {
+      in0 = lane;
+      grp = 0;
+      out0 = (lane & 31) + 512 * (lane >> 5);
+    } else if constexpr (N == 1024) {
       in0 = lane & 31;
       grp = lane >> 5;
       out0 = lane & 31;

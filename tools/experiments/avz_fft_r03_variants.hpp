@@ -1,6 +1,15 @@
 // avz_fft.hpp — wave-level complex FFTs for gfx950 (CDNA4, wave64).
 //
-// Both transforms use exactly ONE LDS transpose:
+// Both transforms hold 16 complex points per lane and use exactly ONE LDS
+// transpose:
+//
+//  Fft1024   : one 1024-point FFT per wave.  N = 32 (n1) x 32 (l).
+//              step 1: 32-pt DFT over n1 = 2r + h  -> 16-pt DFT in registers per
+//                      lane half + one cross-half radix-2 (v_permlane32_swap);
+//              twiddle W1024^{l k1}; LDS transpose (32 x 33 float2, conflict-free);
+//              step 2: same 32-pt structure over l.
+//              in : lane L, reg r  <->  x[64 r + L]
+//              out: lane (k1 = L&31, h = L>>5), reg k'  <->  X[k1 + 32 k' + 512 h]
 //
 //  Fft1024x2 : two independent 1024-point FFTs per wave (lane group g = L>>5),
 //              32 points per lane, NO cross-lane ops: N = 32 (n1, registers) x 32 (l).
@@ -49,8 +58,13 @@ __device__ __forceinline__ cf c_conj(cf a) { return {a.x, -a.y}; }
 // the synthesis kernel's apply and inverse-FFT reads (synthesis 78.3 -> 76.9 us); the
 // analysis kernel's bin-phase and reference-partner reads ran 1 us slower unpaired, and
 // the LDS twiddle reads of Fft1024x2::stage1 spill when unpaired.
+#ifndef AVZ_UNPAIRED
+#define AVZ_UNPAIRED 1
+#endif
 __device__ __forceinline__ cf lds_read(const cf* p) {
+#if AVZ_UNPAIRED
   asm volatile("" ::: "memory");
+#endif
   return *p;
 }
 __device__ __forceinline__ cf c_scale(cf a, float s) { return {a.x * s, a.y * s}; }
@@ -113,6 +127,10 @@ __device__ __forceinline__ void dft4(cf& a0, cf& a1, cf& a2, cf& a3) {
   a3 = {t1.x - t3.y, t1.y + t3.x};  // t1 + i t3
 }
 
+#ifndef AVZ_FFT_TAN
+#define AVZ_FFT_TAN 1
+#endif
+
 // Twiddled radix-2 butterfly y0 = a + w b, y1 = a - w b, w = W32^J (compile time). The
 // non-trivial twiddles run in the tangent form w b = c (b + t (i b)) with |t| <= 1 (t =
 // s / c where |c| >= |s|, else w b = s (t b - i b)-style with t = c / s), so the
@@ -171,6 +189,7 @@ __device__ __forceinline__ void dft16(cf (&v)[16]) {
   static_for<0, 4>([&](auto n2) { dft4(v[n2], v[n2 + 4], v[n2 + 8], v[n2 + 12]); });
   // v[n2 + 4 k1] = B[n2][k1]; twiddle W16^{n2 k1} = W32^{2 n2 k1}
   cf t[16];
+#if AVZ_FFT_TAN
   static_for<0, 4>([&](auto k1) {
     cf a0 = v[0 + 4 * k1], a1 = v[1 + 4 * k1], a2 = v[2 + 4 * k1], a3 = v[3 + 4 * k1];
     dft4_tw<2 * k1>(a0, a1, a2, a3);
@@ -179,11 +198,29 @@ __device__ __forceinline__ void dft16(cf (&v)[16]) {
     t[k1 + 8] = a2;
     t[k1 + 12] = a3;
   });
+#else
+  static_for<1, 4>([&](auto n2) {
+    static_for<1, 4>([&](auto k1) {
+      constexpr int idx = n2 + 4 * k1;
+      v[idx] = w32mul<2 * n2 * k1>(v[idx]);
+    });
+  });
+  // 4-point DFTs over n2 (4 x 4 transpose: v[4 k1 + n2] is B[n2][k1])
+  static_for<0, 4>([&](auto k1) {
+    // B[n2][k1] lives at v[n2 + 4 k1]; DFT along n2 for fixed k1
+    cf a0 = v[0 + 4 * k1], a1 = v[1 + 4 * k1], a2 = v[2 + 4 * k1], a3 = v[3 + 4 * k1];
+    dft4(a0, a1, a2, a3);
+    t[k1 + 0] = a0;   // X[k1 + 4 k2]
+    t[k1 + 4] = a1;
+    t[k1 + 8] = a2;
+    t[k1 + 12] = a3;
+  });
+#endif
   static_for<0, 16>([&](auto i) { v[i] = t[i]; });
 }
 
 // dft16 with emit(k, X[k]) called for the four outputs of each last-stage 4-point DFT as
-// they are formed (v is left holding the last stage's inputs).
+// they are formed (AVZ_FFT_IL; v is left holding the last stage's inputs).
 template <class Emit>
 __device__ __forceinline__ void dft16_emit(cf (&v)[16], Emit&& emit) {
   static_for<0, 4>([&](auto n2) { dft4(v[n2], v[n2 + 4], v[n2 + 8], v[n2 + 12]); });
@@ -229,6 +266,7 @@ __device__ __forceinline__ void xhalf_dit(cf (&v)[16], float sgn, Emit&& emit = 
     float ex, ox, ey, oy;
     xhalf<DIST>(v[k].x, ex, ox);
     xhalf<DIST>(v[k].y, ey, oy);
+#if AVZ_FFT_TAN
     // tangent form: sgn W b = (sgn c)(b + t i b), |t| <= 1 (as bfly_tw)
     constexpr int j = k;
     if constexpr (j == 0 || j == 8) {
@@ -243,6 +281,10 @@ __device__ __forceinline__ void xhalf_dit(cf (&v)[16], float sgn, Emit&& emit = 
       const float m = sgn * (cf_big ? c : s);
       v[k] = {fmaf(m, u.x, ex), fmaf(m, u.y, ey)};
     }
+#else
+    const cf t = w32mul<k>(cf{ox, oy});
+    v[k] = {fmaf(sgn, t.x, ex), fmaf(sgn, t.y, ey)};
+#endif
     if constexpr (EMIT) {
       emit(k, v[k]);
       __builtin_amdgcn_sched_barrier(0);
@@ -259,12 +301,20 @@ __device__ __forceinline__ void dft32(cf (&v)[32]) {
   });
   dft16(e);
   dft16(o);
+#if AVZ_FFT_TAN
   static_for<0, 16>([&](auto k) { bfly_tw<k>(e[k], o[k], v[k], v[k + 16]); });
+#else
+  static_for<0, 16>([&](auto k) {
+    const cf t = w32mul<k>(o[k]);
+    v[k] = c_add(e[k], t);
+    v[k + 16] = c_sub(e[k], t);
+  });
+#endif
 }
 
 // dft32 without its last radix-2 stage: e / o = 16-point DFTs of the even / odd inputs.
 // The callers run the last stage one output pair (k, k + 16) at a time and store each pair
-// as soon as it is formed, behind a scheduling fence, so the LDS stores of a
+// as soon as it is formed (AVZ_FFT_IL), behind a scheduling fence, so the LDS stores of a
 // transpose or spectrum issue between the butterflies instead of as one burst after them.
 __device__ __forceinline__ void dft32_halves(const cf (&v)[32], cf (&e)[16], cf (&o)[16]) {
   static_for<0, 16>([&](auto i) {
@@ -274,6 +324,15 @@ __device__ __forceinline__ void dft32_halves(const cf (&v)[32], cf (&e)[16], cf 
   dft16(e);
   dft16(o);
 }
+#ifndef AVZ_FFT_IL
+#define AVZ_FFT_IL 1
+#endif
+#ifndef AVZ_SIL1_FENCE
+#define AVZ_SIL1_FENCE 1
+#endif
+#ifndef AVZ_IL_TWD
+#define AVZ_IL_TWD 2
+#endif
 
 __device__ __forceinline__ cf unit_root(double frac) {
   // exp(-2 pi i frac), evaluated in fp64 then rounded
@@ -282,7 +341,104 @@ __device__ __forceinline__ cf unit_root(double frac) {
   return {(float)c, (float)(-s)};
 }
 
+// -------------------------------------------------------------------- Fft1024
+struct Fft1024 {
+  static constexpr int N = 1024;
+  static constexpr int PPL = 16;
+  static constexpr int SCRATCH_F2 = 32 * 33;  // float2 elements of LDS scratch
+  cf P[4], Q[4];  // W^{l j} (j<4), W^{l (4 i + 16 h)} (i<4)
+  float sgn;
+  int l, h;
+
+  __device__ __forceinline__ void init(int lane) {
+    l = lane & 31;
+    h = lane >> 5;
+    sgn = h ? -1.0f : 1.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) P[j] = unit_root((double)(l * j) / N);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Q[i] = unit_root((double)(l * (4 * i + 16 * h)) / N);
+  }
+
+  // v: x[64 r + lane] in; X[k1 + 32 r + 512 h] out. scratch: this wave's LDS slot.
+  __device__ __forceinline__ void forward(cf (&v)[16], cf* scratch) const {
+    dft16(v);
+    xhalf_dit<32>(v, sgn);
+    // reg k' holds A[l][k1 = k' + 16 h]; twiddle W1024^{l k1}
+    static_for<0, 16>([&](auto k) {
+      const cf tw = ((k & 3) == 0) ? Q[k >> 2] : c_mul(P[k & 3], Q[k >> 2]);
+      v[k] = c_mul(v[k], tw);
+    });
+    static_for<0, 16>([&](auto k) { scratch[(k + 16 * h) * 33 + l] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = scratch[l * 33 + 2 * r + h]; });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<32>(v, sgn);
+  }
+
+  // Interface shared with Fft1024x2 / Fft512x2 (the chain kernels call these): P and Q
+  // come from a 3 KB block table pq[j][l] (j < 4: W^{l j}; 4 + 4 h + i: W^{l (4 i + 16 h)})
+  // read per transform, so they hold no registers across the kernel's other phases.
+  static constexpr int TW_ENTRIES = 12 * 32;
+  __device__ static void fill_twiddles(cf* tab, int tid, int nthreads) {
+    for (int e = tid; e < TW_ENTRIES; e += nthreads) {
+      const int j = e >> 5, ll = e & 31;
+      const int m = j < 4 ? j : 4 * ((j - 4) & 3) + 16 * ((j - 4) >> 2);
+      tab[e] = unit_root((double)(ll * m) / N);
+    }
+  }
+  __device__ __forceinline__ void forward(cf (&v)[16], cf* scratch, const cf* tab) const {
+    cf p[4], q[4];
+    static_for<0, 4>([&](auto j) {
+      p[j] = tab[j * 32 + l];
+      q[j] = tab[(4 + 4 * h + j) * 32 + l];
+    });
+    dft16(v);
+    xhalf_dit<32>(v, sgn);
+    static_for<0, 16>([&](auto k) {
+      const cf tw = ((k & 3) == 0) ? q[k >> 2] : c_mul(p[k & 3], q[k >> 2]);
+      v[k] = c_mul(v[k], tw);
+    });
+    static_for<0, 16>([&](auto k) { scratch[(k + 16 * h) * 33 + l] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = scratch[l * 33 + 2 * r + h]; });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<32>(v, sgn);
+  }
+  // lane geometry only (the table form needs no P, Q registers)
+  __device__ __forceinline__ void init_lane(int lane) {
+    l = lane & 31;
+    h = lane >> 5;
+    sgn = h ? -1.0f : 1.0f;
+  }
+
+  // The same transform for a lane that did not init(): twiddles W1024^{l k1} come
+  // from a block-shared LDS table tw[k1 * 32 + l] (Fft1024x2::fill_twiddles).
+  __device__ __forceinline__ static void forward_tw(cf (&v)[16], cf* scratch, const cf* tw,
+                                                    int lane) {
+    const int l = lane & 31, h = lane >> 5;
+    const float sg = h ? -1.0f : 1.0f;
+    cf t[16];
+    static_for<0, 16>([&](auto k) { t[k] = lds_read(tw + (k + 16 * h) * 32 + l); });
+    __builtin_amdgcn_sched_barrier(0);  // twiddle reads in flight during the first DFT
+    dft16(v);
+    xhalf_dit<32>(v, sg);
+    static_for<0, 16>([&](auto k) { v[k] = c_mul(v[k], t[k]); });
+    static_for<0, 16>([&](auto k) { scratch[(k + 16 * h) * 33 + l] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = lds_read(scratch + l * 33 + 2 * r + h); });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<32>(v, sg);
+  }
+};
+
 // -------------------------------------------------------------------- Fft1024x2
+#ifndef AVZ_TSTRIDE
+#define AVZ_TSTRIDE 34
+#endif
 struct Fft1024x2 {
   static constexpr int N = 1024;
   static constexpr int PPL = 32;  // points per lane
@@ -290,12 +446,12 @@ struct Fft1024x2 {
   // reads its row back with 16 ds_read_b128 (4 LDS cycles each, conflict-free: row l
   // starts at bank 4 l mod 64) instead of 16 ds_read2_b64 (8 cycles each) at stride 33;
   // the column writes are 128 contiguous bytes per 16 lanes at either stride.
-  static constexpr int TS = 34;
+  static constexpr int TS = AVZ_TSTRIDE;
   static constexpr int GROUP_BYTES = 32 * TS * 8;
   int l;
   // Factored stage-1 twiddles W1024^{l k}, k = 8 m + j: twa[j - 1] = W^{l j} (j < 8),
   // twb[m - 1] = W^{8 l m} (m < 4) — 20 VGPRs in place of the 62 of a full register table
-  // or 31 LDS reads per transform (stage1_ab_st; the synthesis kernel)
+  // or 31 LDS reads per transform (forward_ab; the synthesis kernel)
   cf twa[7], twb[3];
 
   __device__ __forceinline__ void init(int lane) {
@@ -336,8 +492,20 @@ struct Fft1024x2 {
       }
     });
   }
+  // stage1 with the lane's 31 twiddles W1024^{l k1} (k1 = 1..31) held in registers
+  // (tw_reg[k1 - 1]); for kernels with VGPRs to spare, saves 32 LDS reads per FFT pair.
+  __device__ __forceinline__ void stage1_reg(cf (&v)[32], const cf (&tw_reg)[31]) const {
+    dft32(v);
+    static_for<1, 32>([&](auto k) { v[k] = c_mul(v[k], tw_reg[k - 1]); });
+  }
   __device__ __forceinline__ void load_twiddles(cf (&tw_reg)[31], const cf* tw) const {
     static_for<1, 32>([&](auto k) { tw_reg[k - 1] = tw[k * 32 + l]; });
+  }
+  __device__ __forceinline__ void forward_reg(cf (&v)[32], cf* scratch,
+                                              const cf (&tw_reg)[31]) const {
+    stage1_reg(v, tw_reg);
+    transpose(v, scratch);
+    stage2(v);
   }
   __device__ __forceinline__ void transpose(cf (&v)[32], cf* scratch) const {
     static_for<0, 32>([&](auto k) { scratch[k * TS + l] = v[k]; });
@@ -356,7 +524,7 @@ struct Fft1024x2 {
   }
   __device__ __forceinline__ void stage2(cf (&v)[32]) const { dft32(v); }
 
-  // ---- interleaved forms: each output pair (k, k + 16) of a stage's last
+  // ---- interleaved forms (AVZ_FFT_IL): each output pair (k, k + 16) of a stage's last
   // radix-2 is stored the moment it is formed, one pair per scheduling group.
   // Stage 1 with register twiddles -> transpose scratch.
   __device__ __forceinline__ void stage1_reg_st(cf (&v)[32], cf* scratch,
@@ -374,7 +542,7 @@ struct Fft1024x2 {
       // itself (a fence per pair or per 2-4 pairs made it spill 88-152 B)
     });
   }
-  // Stage 1 with the factored register twiddles twa, twb, pairs stored as formed.
+  // Stage 1 with the factored register twiddles (forward_ab's), pairs stored as formed.
   __device__ __forceinline__ void stage1_ab_st(cf (&v)[32], cf* scratch) const {
     cf e[16], o[16];
     dft32_halves(v, e, o);
@@ -390,6 +558,32 @@ struct Fft1024x2 {
       bfly_tw<k>(e[k], o[k], a, b);
       scratch[k * TS + l] = tw(k, a);
       scratch[(k + 16) * TS + l] = tw(std::integral_constant<int, k + 16>{}, b);
+    });
+  }
+  // Stage 1 with the block's LDS twiddle table tw[k1 * 32 + l]: the two twiddles of pair k
+  // are read two pairs ahead.
+  __device__ __forceinline__ void stage1_lds_st(cf (&v)[32], cf* scratch, const cf* tw) const {
+    constexpr int D = AVZ_IL_TWD;  // read distance (pairs)
+    cf ta[D + 1], tb[D + 1];
+    static_for<0, D>([&](auto k) {
+      ta[k] = lds_read(tw + k * 32 + l);
+      tb[k] = lds_read(tw + (k + 16) * 32 + l);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    cf e[16], o[16];
+    dft32_halves(v, e, o);
+    static_for<0, 16>([&](auto k) {
+      if constexpr (k + D < 16) {
+        ta[(k + D) % (D + 1)] = lds_read(tw + (k + D) * 32 + l);
+        tb[(k + D) % (D + 1)] = lds_read(tw + (k + D + 16) * 32 + l);
+      }
+      cf a, b;
+      bfly_tw<k>(e[k], o[k], a, b);
+      if constexpr (k > 0) a = c_mul(a, ta[k % (D + 1)]);
+      b = c_mul(b, tb[k % (D + 1)]);
+      scratch[k * TS + l] = a;
+      scratch[(k + 16) * TS + l] = b;
+      if constexpr (AVZ_SIL1_FENCE) __builtin_amdgcn_sched_barrier(0);
     });
   }
   // Rows of the transpose back into registers (after a stage1_*_st).
@@ -416,6 +610,25 @@ struct Fft1024x2 {
       emit(std::integral_constant<int, k + 16>{}, v[k + 16]);
       __builtin_amdgcn_sched_barrier(0);
     });
+  }
+  // stage 1 with the factored twiddles: W^{l (8 m + j)} v = W^{8 l m} (W^{l j} v)
+  __device__ __forceinline__ void stage1_ab(cf (&v)[32]) const {
+    dft32(v);
+    static_for<1, 32>([&](auto k) {
+      constexpr int j = k & 7, m = k >> 3;
+      if constexpr (m == 0) {
+        v[k] = c_mul(v[k], twa[j - 1]);
+      } else if constexpr (j == 0) {
+        v[k] = c_mul(v[k], twb[m - 1]);
+      } else {
+        v[k] = c_mul(c_mul(v[k], twa[j - 1]), twb[m - 1]);
+      }
+    });
+  }
+  __device__ __forceinline__ void forward_ab(cf (&v)[32], cf* scratch) const {
+    stage1_ab(v);
+    transpose(v, scratch);
+    stage2(v);
   }
   __device__ __forceinline__ void forward(cf (&v)[32], cf* scratch, const cf* tw) const {
     stage1(v, tw);
@@ -452,7 +665,7 @@ struct Fft512x2 {
   __device__ static void fill_twiddles(cf*, int, int) {}
 
   // forward with the transpose stores issued as stage 1's outputs are formed and emit(k,
-  // X_g[k1 + 16 k + 256 h]) called for each output of stage 2 as it is formed
+  // X_g[k1 + 16 k + 256 h]) called for each output of stage 2 as it is formed (AVZ_FFT_IL)
   template <class Emit>
   __device__ __forceinline__ void forward_emit(cf (&v)[16], cf* scratch, Emit&& emit) const {
     dft16_emit(v, [&](auto k, cf x) {
@@ -478,6 +691,30 @@ struct Fft512x2 {
     xhalf_dit<16>(v, sgn);
   }
 
+  // The same transform for a lane that did not init(), with its W512 twiddles read from
+  // Fft1024x2's block table tw[k1 * 32 + l] = W1024^{l k1}: W512^{j i} = tw[2 i][j],
+  // W512^{4 j i} = tw[8 i][j] (the 1024-point synthesis runs its inverse at N/2).
+  __device__ __forceinline__ static void forward_tw1024(cf (&v)[16], cf* scratch, const cf* tw,
+                                                        int lane) {
+    const int jj = lane & 31, kk = lane & 15, hh = (lane >> 4) & 1;
+    const float sg = hh ? -1.0f : 1.0f;
+    cf p[4], q[4];
+    static_for<0, 4>([&](auto i) {
+      p[i] = lds_read(tw + (2 * i) * 32 + jj);
+      q[i] = lds_read(tw + (8 * i) * 32 + jj);
+    });
+    dft16(v);
+    static_for<1, 16>([&](auto k) {
+      const cf t = ((k & 3) == 0) ? q[k >> 2] : c_mul(p[k & 3], q[k >> 2]);
+      v[k] = c_mul(v[k], t);
+    });
+    static_for<0, 16>([&](auto k) { scratch[k * 34 + jj] = v[k]; });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = scratch[kk * 34 + 2 * r + hh]; });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<16>(v, sg);
+  }
 };
 
 }  // namespace avz
