@@ -21,10 +21,14 @@ import torch  # noqa: E402
 import avz  # noqa: E402
 from avz import synth  # noqa: E402
 
-# avz_chunked.hip stamp slots: analysis 0-3, 11, 12; synthesis 4-10
+# avz_chunked.hip stamp slots: analysis 0-3, 11, 12; synthesis 4-10; the role-split
+# synthesis (--rs): producer wave 4-7, consumer wave 8-10, 13-15
 PHASES = ["A load wait", "A barrier 1", "A barrier 2", "A window+FFT", "S prologue",
           "S load wait", "S FFT", "S apply", "S iFFT", "S OLA", "S peak", "A load issue",
-          "A bins"]
+          "A bins", "-", "-", "-"]
+RS_PHASES = {4: "P prologue", 5: "P window+FFT", 6: "P next loads", 7: "P barrier",
+             8: "C apply", 9: "C iFFT", 10: "C sync wait", 13: "C OLA", 14: "C barrier",
+             15: "C item coefs"}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=256)
@@ -32,7 +36,11 @@ ap.add_argument("--n-fft", type=int, default=1024)
 ap.add_argument("--mask", default="ibm")
 ap.add_argument("--normalize", default="peak")
 ap.add_argument("--seconds", type=float, default=4.0)
+ap.add_argument("--synth-variant", type=int, default=-1, help="avz_debug_set_synth_variant")
 a = ap.parse_args()
+if a.synth_variant >= 0:
+    PHASES = [RS_PHASES.get(i, n) if i >= 4 and a.synth_variant == 1 else n
+              for i, n in enumerate(PHASES)]
 S = int(a.seconds * 16000)
 dev = torch.device("cuda:0")
 mix, tgt, itf = synth.make_batch(a.batch, n_samples=S, n_interferers=2)
@@ -44,6 +52,8 @@ kw = dict(ref_tgt=d[1], ref_int=d[2]) if a.mask == "ibm" else {}
 nblk = a.batch * -(-plan.frames(S) // avz._lib.lib.avz_chunk_frames())
 st = torch.zeros((nblk, 16), dtype=torch.int64, device=dev)
 lib = avz._lib.lib
+if a.synth_variant >= 0:
+    lib.avz_debug_set_synth_variant(a.synth_variant)
 setter = lib.avz_debug_set_stamps_chunked
 setter.argtypes = [ct.c_void_p]
 for _ in range(3):
