@@ -38,6 +38,8 @@ namespace avz {
 // this file holds only the shipped paths.
 
 constexpr int kChunk = 32;      // frames per chunk = bits of one mask word
+constexpr int kSC1 = 16;        // buffer-op cache policy bit: sc1 (L1-bypassing loads, gfx940+)
+typedef int v4i_t __attribute__((ext_vector_type(4)));
 constexpr int kCThreads = 256;  // 4 waves
 
 template <int N>
@@ -1235,6 +1237,331 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_syn
     synthesis_item<N, PF, SPEC>(A, lds, it % gx, it / gx, K);
 }
 
+// ============================ per-utterance synthesis (N = 1024) ============================
+// One 8-wave block per CU synthesises WHOLE utterances (b = blockIdx.x, + gridDim.x, ...),
+// 16 frames per step, and peak-normalises each one itself at its end: no chunk seams, no
+// heads / tails, no finalize launch, and the rescale re-reads the block's own output from
+// L2 / Infinity Cache instead of a second HBM pass over the batch. Every wave runs its own
+// two frames end to end -- window + forward Fft1024x2 (the next step's loads issued from
+// inside its last stage), apply w^H y + post-filter, each frame's real inverse as an
+// N/2-point complex Fft512x2 -- with no block barrier in between (the apply reads only the
+// wave's own spectra); the block meets twice per step, around the overlap-add of the 16
+// segments, which reads neighbouring waves' frames. Reference semantics as the two-block
+// kernel + avz_finalize_kernel (oracle_debug.py:80-94, scipy istft's OLA and N/2 trim).
+#ifndef AVZ_UTT_LOADS
+#define AVZ_UTT_LOADS 2
+#endif
+constexpr int kUttThreads = 512;
+struct UttGeo {
+  static constexpr int N = 1024, H = 512, F = 513, FB = 16;  // frames per step: 8 waves x 2
+  static constexpr int SLOT = KCfg<1024>::GROUP_BYTES;       // one frame (transpose rows of 34)
+  static constexpr int TW_OFF = FB * SLOT;                   // W1024 table (Fft512x2 inverse)
+  static constexpr int COEF_OFF = TW_OFF + KCfg<1024>::TW_BYTES;  // the utterance's alpha, beta
+  static constexpr int RED_OFF = COEF_OFF + F * 16;
+  static constexpr int LDS_BYTES = RED_OFF + 64;
+  static_assert(LDS_BYTES <= 160 * 1024, "one block per CU");
+  static_assert(kChunk % FB == 0, "a step stays inside one 32-frame mask chunk");
+};
+__device__ __forceinline__ cf* utt_frame(unsigned char* lds, int f) {
+  return reinterpret_cast<cf*>(lds + f * UttGeo::SLOT);
+}
+
+template <int PF>
+__global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(ChainArgs A) {
+  constexpr int N = UttGeo::N, H = UttGeo::H, F = UttGeo::F, FB = UttGeo::FB;
+  extern __shared__ __align__(16) unsigned char lds[];
+  cf* twid = reinterpret_cast<cf*>(lds + UttGeo::TW_OFF);
+  float* red = reinterpret_cast<float*>(lds + UttGeo::RED_OFF);
+  Fft1024x2::fill_twiddles(twid, threadIdx.x, kUttThreads);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // 0..7
+  const int lane = tid & 63;
+  Fft1024x2 fft;
+  fft.init(lane);
+  LaneMap<N> lm;
+  lm.init(lane);
+  const WinCoef<N> wc0 = [&] { WinCoef<N> w; w.init(lm); return w; }();
+  const int my = 2 * wave + lm.grp;  // frame of the step = slot
+  // apply bins: m_j = lane + 64 j (j < 4) pairs bin kA = m with kB = N/2 - m; bin N/4 (its
+  // own partner) on lanes 0 (frame 2 wave) and 1 (frame 2 wave + 1)
+  cf om[4];  // e^{+2 pi i m_j / N}
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double sn, cs;
+    sincospi(2.0 * (lane + 64 * j) / N, &sn, &cs);
+    om[j] = cf{(float)cs, (float)sn};
+  }
+  // inverse output: x[k] = conj(z[m]), m = mh + 16 k -> samples 2m, 2m + 1 (0.5 hann)
+  float wh_c[2], wh_s[2];
+  const int mh = (lane & 15) + 256 * ((lane >> 4) & 1);
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    double sn, cs;
+    sincospi(2.0 * (2 * mh + e) / N, &sn, &cs);
+    wh_c[e] = (float)(0.25 * cs);
+    wh_s[e] = (float)(0.25 * sn);
+  }
+  // overlap-add role: 4 consecutive samples m0.. of segments sgrp + 4 si
+  float inv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(4 * (tid & 127) + i);
+  const rsrc_t r_none = make_rsrc(nullptr, 0);
+  __syncthreads();  // twiddle table
+
+  // the block's utterances b = blockIdx.x, + gridDim.x, ...; one with a bad device length
+  // (host validates) reports NaN, as finalize does, and is skipped
+  auto next_valid = [&](int bb) {
+    for (; bb < A.batch; bb += gridDim.x) {
+      if (utt_len(A, bb) >= N) break;
+      if (tid == 0 && A.peak) A.peak[bb] = __builtin_nanf("");
+    }
+    return bb;
+  };
+  auto rsrcs = [&](int bb, rsrc_t& a0, rsrc_t& a1) {
+    const float* mixb = A.mix + (long long)bb * A.mix_stride;
+    const int len = utt_len(A, bb);
+    a0 = make_rsrc(mixb, len);
+    a1 = make_rsrc(mixb + A.ch_stride, len);
+  };
+  cf v[32];
+  // step 0 of an utterance: wave 0's first frame starts N/2 before sample 0 (range-checked
+  // offsets); the other waves' frames start at sample >= 0
+  auto first_loads = [&](rsrc_t a0, rsrc_t a1) {
+    const int s0 = my * H - N / 2 + lm.in0;
+    if (wave >= 1) {
+      static_for<0, 32>([&](auto r) {
+        v[r].x = bload_nn(a0, s0 + 32 * r);
+        v[r].y = bload_nn(a1, s0 + 32 * r);
+      });
+    } else {
+      static_for<0, 32>([&](auto r) {
+        v[r].x = bload(a0, s0 + 32 * r);
+        v[r].y = bload(a1, s0 + 32 * r);
+      });
+    }
+  };
+  int b = next_valid(blockIdx.x);
+  if (b < A.batch) {
+    rsrc_t a0, a1;
+    rsrcs(b, a0, a1);
+    first_loads(a0, a1);
+  }
+  while (b < A.batch) {
+    const int L = utt_len(A, b);
+    const int T = (L + H - 1) / H + 1;
+    const int nstep = (T + FB - 1) / FB;
+    rsrc_t r0, r1;
+    rsrcs(b, r0, r1);
+    // the next utterance's first step is loaded during this one's last step (waves >= 1
+    // from inside the FFT, wave 0 right after it) and lands during the rescale
+    const int nb = next_valid(b + gridDim.x);
+    rsrc_t n0 = r_none, n1 = r_none;
+    if (nb < A.batch) rsrcs(nb, n0, n1);
+    // the utterance's apply coefficients into LDS (read per step, so they hold no registers
+    // through the FFTs); the previous utterance's readers finished at its last barrier
+    {
+      const float4* coef = reinterpret_cast<const float4*>(A.coef) + (long long)b * F;
+      float4* ct = reinterpret_cast<float4*>(lds + UttGeo::COEF_OFF);
+      for (int k = tid; k < F; k += kUttThreads) ct[k] = coef[k];
+    }
+    __syncthreads();
+    uint32_t bits[9];
+    float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);
+    float peak = 0.0f;
+    float* outb = A.out + (long long)b * A.out_stride;
+    for (int step = 0; step < nstep; ++step) {
+      const int f0 = step * FB, c = f0 / kChunk;
+      // lane-derived LDS / global offsets recomputed per step (held across the loop they
+      // cost ~100 VGPRs and spilled)
+      int ln = lane, tq = tid;
+      opaque_i(ln);
+      opaque_i(tq);
+      if (f0 % kChunk == 0 && PF == PF_IBM_TARGET) {  // the chunk's post-filter bits
+        const uint32_t* MW = A.mwords + ((long long)b * A.nchunk + c) * F;
+#pragma unroll
+        for (int q = 0; q < 9; ++q)
+          bits[q] = MW[q < 4 ? ln + 64 * q : (q < 8 ? H - ln - 64 * (q - 4) : N / 4)];
+      }
+      // ---- window + forward FFT of frames f0 + 2 wave + g into slot my; the next step's
+      // loads go out from inside its last stage (frames >= FB: no negative sample index)
+      const bool more = step + 1 < nstep;
+      const bool il = more || wave >= 1;
+      const rsrc_t q0 = more ? r0 : (wave >= 1 ? n0 : r_none);
+      const rsrc_t q1 = more ? r1 : (wave >= 1 ? n1 : r_none);
+      const int sn = ((more ? f0 + FB : 0) + my) * H - N / 2 + lm.in0;
+      // AVZ_UTT_LOADS (experiment): where the next step's loads are issued -- 0 from inside
+      // the forward FFT's last stage, 1 after the FFT, 2 after the apply, 3 after the inverse
+      auto next_loads = [&]() {
+        if (il) {
+          static_for<0, 32>([&](auto k) {
+            v[k].x = bload_nn(q0, sn + 32 * k);
+            v[k].y = bload_nn(q1, sn + 32 * k);
+          });
+        } else {
+          first_loads(n0, n1);  // wave 0, last step: the next utterance (or empty)
+        }
+      };
+      if constexpr (AVZ_UTT_LOADS == 0) {
+        window_fft<N>(v, wc0, fft, utt_frame(lds, my), lm, [&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          v[k].x = bload_nn(q0, sn + 32 * k);
+          v[k].y = bload_nn(q1, sn + 32 * k);
+        });
+        if (!il) first_loads(n0, n1);
+      } else {
+        window_fft<N>(v, wc0, fft, utt_frame(lds, my), lm);
+        if (AVZ_UTT_LOADS == 1) next_loads();
+      }
+      __builtin_amdgcn_wave_barrier();
+      const float* irm = (PF == PF_IRM) ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F
+                                        : nullptr;
+      auto gain = [&](uint32_t bb, int i, int t, int k) -> float {  // i: frame bit in chunk
+        if (t >= T) return 0.0f;
+        if constexpr (PF == PF_IBM_TARGET) {
+          return ((bb >> i) & 1u) ? 0.0f : 1.0f;
+        } else if constexpr (PF == PF_IRM) {
+          return irm[i * F + k];
+        } else if constexpr (PF == PF_EXT_FLOOR || PF == PF_EXT_MUL) {
+          const float M = A.ext_mask[(long long)b * A.mask_sb + (long long)k * A.mask_sf +
+                                     (long long)t * A.mask_st];
+          return PF == PF_EXT_FLOOR ? fmaxf(M, A.pf_floor) : M;
+        } else {
+          return 1.0f;
+        }
+      };
+      // ---- apply w^H y + post-filter of the wave's frames, folded into each frame's
+      // N/2-point inverse input (written in place over the bins just read):
+      //   Zh[m] = A + i B, Zh[N/2 - m] = conj(A) + i conj(B),
+      //   A = S[m] + conj(S[N/2 - m]),  B = e^{2 pi i m / N} (S[m] - conj(S[N/2 - m]))
+      cf al[9], be[9];
+      {
+        const float4* ct = reinterpret_cast<const float4*>(lds + UttGeo::COEF_OFF);
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+          const float4 w = ct[q < 4 ? ln + 64 * q : (q < 8 ? H - ln - 64 * (q - 4) : N / 4)];
+          al[q] = cf{w.x, w.y};
+          be[q] = cf{w.z, w.w};
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int f = 2 * wave + g, t = f0 + f, ib = f0 % kChunk + f;
+        cf* Z = utt_frame(lds, f);
+        cf za[4], zap[4], zb[4], zbp[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kA = ln + 64 * j, kB = H - kA;
+          za[j] = lds_read(Z + kA);
+          zap[j] = lds_read(Z + ((N - kA) & (N - 1)));
+          zb[j] = lds_read(Z + kB);
+          zbp[j] = lds_read(Z + (N - kB));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kA = ln + 64 * j, kB = H - kA;
+          cf sa = apply_bin(al[j], be[j], za[j], zap[j], gain(bits[j], ib, t, kA));
+          cf sb = apply_bin(al[4 + j], be[4 + j], zb[j], zbp[j], gain(bits[4 + j], ib, t, kB));
+          if (j == 0 && ln == 0) {  // DC and Nyquist: irfft keeps the real parts
+            sa.y = 0.0f;
+            sb.y = 0.0f;
+          }
+          const cf a = {sa.x + sb.x, sa.y - sb.y};
+          const cf d = {sa.x - sb.x, sa.y + sb.y};
+          const cf bb = c_mul(om[j], d);
+          Z[kA] = {a.x - bb.y, a.y + bb.x};
+          Z[kB] = {a.x + bb.y, bb.x - a.y};
+        }
+        if (ln == g) {  // bin N/4: Zh = 2 conj(S)
+          const cf s = apply_bin(al[8], be[8], Z[N / 4], Z[3 * N / 4], gain(bits[8], ib, t, N / 4));
+          Z[N / 4] = {2.0f * s.x, -2.0f * s.y};
+        }
+      }
+      if (AVZ_UTT_LOADS == 2) next_loads();
+      __builtin_amdgcn_wave_barrier();
+      // ---- inverse: lane group g transforms frame 2 wave + g; windowed contributions
+      // (samples 2m, 2m + 1 as one float2) over the frame's first 4 KB, the transpose in its
+      // second half
+      {
+        cf* Zi = utt_frame(lds, my);
+        cf u[16];
+        static_for<0, 16>([&](auto r) { u[r] = c_conj(lds_read(Zi + (ln & 31) + 32 * r)); });
+        float2* Cp = reinterpret_cast<float2*>(Zi);
+        const int mhs = (ln & 15) + 256 * ((ln >> 4) & 1);
+        Fft512x2::forward_tw1024_emit(u, Zi + H, twid, ln, [&](auto k, cf x) {
+          constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi (32 k) / N
+          const float we = fmaf(wh_s[0], sk, fmaf(-wh_c[0], ck, 0.25f));
+          const float wo = fmaf(wh_s[1], sk, fmaf(-wh_c[1], ck, 0.25f));
+          Cp[mhs + 16 * k] = make_float2(x.x * we, -x.y * wo);
+        });
+      }
+      if (AVZ_UTT_LOADS == 3) next_loads();
+      lds_barrier();
+      // ---- overlap-add: segment j = f0 - 1 + s = frame s-1 (2nd half) + frame s (1st half);
+      // segment -1 (frame 0's first half) is scipy's trimmed N/2
+      auto cframe = [&](int f) -> const float* {
+        return reinterpret_cast<const float*>(utt_frame(lds, f));
+      };
+      const int m0 = 4 * (tq & 127), sgrp = __builtin_amdgcn_readfirstlane(tq >> 7);
+#pragma unroll
+      for (int si = 0; si < 4; ++si) {
+        const int s = sgrp + 4 * si;
+        const int j = f0 - 1 + s;
+        if (j >= 0 && j <= T - 2) {
+          const float4 vb = *reinterpret_cast<const float4*>(cframe(s) + m0);
+          float4 va = carry;  // a select of values, not of pointers (that put carry on the stack)
+          if (s != 0) va = *reinterpret_cast<const float4*>(cframe(s - 1) + H + m0);
+          float4 o;
+          o.x = (va.x + vb.x) * inv[0];
+          o.y = (va.y + vb.y) * inv[1];
+          o.z = (va.z + vb.z) * inv[2];
+          o.w = (va.w + vb.w) * inv[3];
+          *reinterpret_cast<float4*>(outb + (long long)j * H + m0) = o;
+          peak = fmaxf(peak, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+        }
+      }
+      if (sgrp == 0) carry = *reinterpret_cast<const float4*>(cframe(FB - 1) + H + m0);
+      lds_barrier();
+    }
+    // ---- utterance peak; NORM_PEAK rescales the block's own output (its stores drained
+    // first; L1-bypassing loads), as avz_finalize_kernel did in a second pass over HBM
+    for (int o = 32; o > 0; o >>= 1) peak = fmaxf(peak, __shfl_xor(peak, o, 64));
+    if (lane == 0) red[wave] = peak;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float pk = red[0];
+#pragma unroll
+    for (int w = 1; w < kUttThreads / 64; ++w) pk = fmaxf(pk, red[w]);
+    if (tid == 0 && A.peak) A.peak[b] = pk;
+    if (A.normalize == NORM_PEAK) {
+      const float scale = 1.0f / (pk + A.norm_eps);
+      const int n4 = (T - 1) * H / 4;
+      const rsrc_t ro = make_rsrc(outb, (long long)(T - 1) * H);
+      float4* o4 = reinterpret_cast<float4*>(outb);
+      constexpr int U = 8;  // float4 loads in flight per thread
+      for (int base = 0; base < n4; base += U * kUttThreads) {
+        float4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const v4i_t d = __builtin_amdgcn_raw_buffer_load_b128(
+              ro, 16 * (base + u * kUttThreads + tid), 0, kSC1);
+          x[u] = make_float4(__int_as_float(d.x), __int_as_float(d.y), __int_as_float(d.z),
+                             __int_as_float(d.w));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = base + u * kUttThreads + tid;
+          if (i < n4) {
+            x[u].x *= scale; x[u].y *= scale; x[u].z *= scale; x[u].w *= scale;
+            o4[i] = x[u];
+          }
+        }
+      }
+    }
+    __syncthreads();  // red[] of the next utterance
+    b = nb;
+  }
+}
+
 // ================================ finalize ================================
 // Finalize blocks handle FCH consecutive chunks (N = 512: two, so a block rescales the same
 // 64 KB as N = 1024's one chunk instead of twice as many blocks moving 31 KB each).
@@ -1360,8 +1687,53 @@ extern "C" int avz_chunk_frames(void) { return kChunk; }
 
 static int resident_cus();
 
-// The synthesis launch of the chain and of the stage exports (persistent grid).
+// Synthesis kernel selection (diagnostic A/B, avz_debug_set_synth_variant): 1 = the
+// per-utterance kernel for N = 1024 time-domain input (no finalize launch), 0 = the
+// two-block chunk kernel + avz_finalize_kernel.
+static std::atomic<int> g_synth_variant{1};
+extern "C" int avz_debug_set_synth_variant(int v) {
+  if (v < 0 || v > 1) return -1;
+  g_synth_variant.store(v);
+  return 0;
+}
+// The per-utterance kernel covers the IBM-target and unfiltered post-filters (the headline
+// and the IPD configuration); the IRM and external-mask gains, read per (bin, frame) from
+// memory, need registers it does not have (48-56 B of scratch), so those plans keep the
+// chunk grid + finalize.
+template <int N, int PF, bool SPEC>
+static bool synth_per_utterance() {
+  return N == 1024 && !SPEC && (PF == PF_IBM_TARGET || PF == PF_NONE) &&
+         g_synth_variant.load(std::memory_order_relaxed) == 1;
+}
+
+// Synthesis + output normalisation of the chain and of the stage exports: the per-utterance
+// kernel (N = 1024, time-domain input; finalize events record an empty span), or the
+// persistent chunk grid followed by avz_finalize_kernel.
 template <int N, int PF, bool SPEC = false>
+static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
+template <int N, int PF, bool SPEC = false>
+static int launch_synth_finalize(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1,
+                                 hipEvent_t e2, hipEvent_t e3) {
+  if (synth_per_utterance<N, PF, SPEC>()) {
+    constexpr int lds = UttGeo::LDS_BYTES;
+    constexpr int UPF = (PF == PF_IBM_TARGET || PF == PF_NONE) ? PF : PF_NONE;  // instantiated
+    if (!lds_ready<avz_synthesis_utt_kernel<UPF>>(lds)) return -3;
+    const dim3 grid((unsigned)std::min(a->batch, resident_cus()));
+    hipExtLaunchKernelGGL((avz_synthesis_utt_kernel<UPF>), grid, dim3(kUttThreads), lds, st, e0,
+                          e1, 0, *a);
+    if (e2 && (hipEventRecord(e2, st) != hipSuccess || hipEventRecord(e3, st) != hipSuccess))
+      return -3;
+    return 0;
+  }
+  if (launch_synthesis<N, PF, SPEC>(a, st, e0, e1) != 0) return -3;
+  const int nch = (a->max_frames + kChunk - 1) / kChunk;
+  hipExtLaunchKernelGGL(avz_finalize_kernel<N>, dim3(fin_groups<N>(nch), a->batch), dim3(kCThreads),
+                        0, st, e2, e3, 0, *a);
+  return 0;
+}
+
+// The synthesis launch of the chain and of the stage exports (persistent grid).
+template <int N, int PF, bool SPEC>
 static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   constexpr int lds = SGeo<N, kSynR<N, PF>>::LDS_BYTES;
@@ -1421,9 +1793,8 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   } else {
     hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), evt(3), 0, *a);
   }
-  if (launch_synthesis<N, PF>(a, st, evt(4), evt(5)) != 0) return -3;
-  hipExtLaunchKernelGGL(k3, dim3(fin_groups<N>(nch), a->batch), dim3(kCThreads), 0, st, evt(6),
-                        evt(7), 0, *a);
+  (void)k3;
+  if (launch_synth_finalize<N, PF>(a, st, evt(4), evt(5), evt(6), evt(7)) != 0) return -3;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -1538,10 +1909,7 @@ static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
   if (a->peak && a->normalize != NORM_PEAK &&
       hipMemsetAsync(a->peak, 0, sizeof(float) * a->batch, st) != hipSuccess)
     return -3;
-  // one synthesis launch over the batch, then the finalize kernel
-  if (launch_synthesis<N, PF, SPEC>(a, st, nullptr, nullptr) != 0) return -3;
-  hipLaunchKernelGGL(avz_finalize_kernel<N>, dim3(fin_groups<N>(nch), a->batch), dim3(kCThreads), 0,
-                     st, *a);
+  if (launch_synth_finalize<N, PF, SPEC>(a, st, nullptr, nullptr, nullptr, nullptr) != 0) return -3;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

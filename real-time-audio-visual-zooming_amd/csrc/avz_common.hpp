@@ -60,6 +60,7 @@ __device__ __forceinline__ float bload_nn(rsrc_t r, int elem) {
 // lane-constant terms (window weights) then stays in the loop instead of being hoisted
 // out and held in (or spilled from) registers for the whole kernel.
 __device__ __forceinline__ void opaque(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void opaque_i(int& x) { asm volatile("" : "+v"(x)); }
 
 // LDS-only barrier: leaves global loads (the next frame's prefetch) in flight.
 __device__ __forceinline__ void lds_barrier() {

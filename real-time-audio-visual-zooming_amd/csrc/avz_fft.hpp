@@ -466,6 +466,32 @@ struct Fft512x2 {
     xhalf_dit<16>(v, sgn, emit);
   }
 
+  // forward_emit for a lane that did not init(): the W512 twiddles come from Fft1024x2's
+  // block table tw[k1 * 32 + l] = W1024^{l k1} (W512^{j i} = tw[2 i][j], W512^{4 j i} =
+  // tw[8 i][j]), formed per transform as init() forms them (same rounding); the N = 1024
+  // per-utterance synthesis runs each frame's real inverse at N/2 with it.
+  template <class Emit>
+  __device__ __forceinline__ static void forward_tw1024_emit(cf (&v)[16], cf* scratch, const cf* tw,
+                                                             int lane, Emit&& emit) {
+    const int jj = lane & 31, kk = lane & 15, hh = (lane >> 4) & 1;
+    const float sg = hh ? -1.0f : 1.0f;
+    cf p[4], q[4];
+    static_for<0, 4>([&](auto i) {
+      p[i] = lds_read(tw + (2 * i) * 32 + jj);
+      q[i] = lds_read(tw + (8 * i) * 32 + jj);
+    });
+    dft16_emit(v, [&](auto k, cf x) {
+      constexpr int kc = decltype(k)::value;
+      if constexpr (kc > 0) x = c_mul(x, ((kc & 3) == 0) ? q[kc >> 2] : c_mul(p[kc & 3], q[kc >> 2]));
+      scratch[kc * 34 + jj] = x;
+    });
+    __builtin_amdgcn_wave_barrier();
+    static_for<0, 16>([&](auto r) { v[r] = scratch[kk * 34 + 2 * r + hh]; });
+    __builtin_amdgcn_wave_barrier();
+    dft16(v);
+    xhalf_dit<16>(v, sg, emit);
+  }
+
   // v: x_g[j + 32 r] in; X_g[k1 + 16 r + 256 h] out. scratch: this lane group's slot.
   __device__ __forceinline__ void forward(cf (&v)[16], cf* scratch, const cf* = nullptr) const {
     dft16(v);  // reg k holds A[j][k]
