@@ -37,6 +37,9 @@ namespace avz {
 // stage-1 stores, ...) are recorded in DESIGN.md §6 and kept under tools/experiments/;
 // this file holds only the shipped paths.
 
+#ifndef AVZ_REF_HALF
+#define AVZ_REF_HALF 0
+#endif
 constexpr int kChunk = 32;      // frames per chunk = bits of one mask word
 constexpr int kSC1 = 16;        // buffer-op cache policy bit: sc1 (L1-bypassing loads, gfx940+)
 typedef int v4i_t __attribute__((ext_vector_type(4)));
@@ -189,6 +192,26 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
   const int l = lm.out0;
   fft.stage1_reg_st(v, spec, tw_reg);
   fft.transpose_read(v, spec);
+#if AVZ_REF_HALF
+  // experiment: only the upper-half outputs stored (their registers reload during the
+  // stage), the lower half kept for the bits and reloaded after them
+  fft.stage2_emit(v, [&](auto k, cf x) {
+    if constexpr (decltype(k)::value >= 16) {
+      spec[l + 32 * k] = x;
+      after(k);
+    }
+  });
+  __builtin_amdgcn_wave_barrier();
+  uint32_t w = 0u;
+  static_for<0, 16>([&](auto k) {
+    const int m = l + 32 * k;
+    cf zp = spec[(N - m) & (N - 1)];
+    if (k == 0 && l == 0) zp = v[0];  // DC: its own partner (index 0 is not stored)
+    w |= (ibm_noise(v[k], zp) ? 1u : 0u) << k;
+  });
+  reinterpret_cast<uint32_t*>(spec)[l] = w;
+  static_for<0, 16>([&](auto k) { after(k); });
+#else
   fft.stage2_emit(v, [&](auto k, cf x) {
     spec[l + 32 * k] = x;
     after(k);
@@ -203,6 +226,7 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
   });
   static_for<0, 16>([&](auto k) { w |= (ibm_noise(zo[k], zp[k]) ? 1u : 0u) << k; });
   reinterpret_cast<uint32_t*>(spec)[l] = w;
+#endif
 }
 
 // Window + forward FFT of the synthesis kernel and of the N = 512 analysis kernel:
@@ -1346,6 +1370,43 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     rsrcs(b, a0, a1);
     first_loads(a0, a1);
   }
+  // NORM_PEAK: an utterance's rescale (its own output, L1-bypassing loads) runs spread over
+  // the NEXT utterance's steps, one slice per overlap-add phase, so its memory traffic hides
+  // under that utterance's FFTs; a block's last utterance rescales at once.
+  float* rs_out = nullptr;  // pending rescale: output row, scale, float4 groups, done
+  float rs_scale = 0.0f;
+  int rs_n4 = 0, rs_done = 0;
+  constexpr int RS_U = 4;   // float4 groups per thread per slice (8 slices cover 4 s)
+  constexpr int RS_BULK = 32;  // after the loop: a 4-s utterance in one round trip of loads
+  auto rescale_slice = [&](auto uc, int lo, int hi, auto issue_more) {
+    constexpr int U = decltype(uc)::value;
+    const rsrc_t ro = make_rsrc(rs_out, 4LL * rs_n4);
+    float4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const v4i_t d = __builtin_amdgcn_raw_buffer_load_b128(ro, 16 * (lo + u * kUttThreads + tid), 0,
+                                                            kSC1);
+      x[u] = make_float4(__int_as_float(d.x), __int_as_float(d.y), __int_as_float(d.z),
+                         __int_as_float(d.w));
+    }
+    issue_more();  // work that overlaps the loads
+    float4* o4 = reinterpret_cast<float4*>(rs_out);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = lo + u * kUttThreads + tid;
+      if (i < hi) {
+        x[u].x *= rs_scale; x[u].y *= rs_scale; x[u].z *= rs_scale; x[u].w *= rs_scale;
+        o4[i] = x[u];
+      }
+    }
+  };
+  // the pending rescale's remaining part, U float4 loads per thread in flight
+  auto rescale_rest = [&](auto uc) {
+    constexpr int U = decltype(uc)::value;
+    for (; rs_done < rs_n4; rs_done += U * kUttThreads)
+      rescale_slice(uc, rs_done, min(rs_n4, rs_done + U * kUttThreads), [] {});
+    rs_out = nullptr;
+  };
   while (b < A.batch) {
     const int L = utt_len(A, b);
     const int T = (L + H - 1) / H + 1;
@@ -1502,6 +1563,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         return reinterpret_cast<const float*>(utt_frame(lds, f));
       };
       const int m0 = 4 * (tq & 127), sgrp = __builtin_amdgcn_readfirstlane(tq >> 7);
+      auto ola = [&]() {
 #pragma unroll
       for (int si = 0; si < 4; ++si) {
         const int s = sgrp + 4 * si;
@@ -1519,6 +1581,14 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
           peak = fmaxf(peak, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
         }
       }
+      };
+      if (rs_out != nullptr && rs_done < rs_n4) {  // a slice of the previous utterance's rescale
+        const int lo = rs_done, hi = min(rs_n4, rs_done + RS_U * kUttThreads);
+        rescale_slice(std::integral_constant<int, RS_U>{}, lo, hi, ola);
+        rs_done = hi;
+      } else {
+        ola();
+      }
       if (sgrp == 0) carry = *reinterpret_cast<const float4*>(cframe(FB - 1) + H + m0);
       lds_barrier();
     }
@@ -1533,33 +1603,20 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     for (int w = 1; w < kUttThreads / 64; ++w) pk = fmaxf(pk, red[w]);
     if (tid == 0 && A.peak) A.peak[b] = pk;
     if (A.normalize == NORM_PEAK) {
-      const float scale = 1.0f / (pk + A.norm_eps);
-      const int n4 = (T - 1) * H / 4;
-      const rsrc_t ro = make_rsrc(outb, (long long)(T - 1) * H);
-      float4* o4 = reinterpret_cast<float4*>(outb);
-      constexpr int U = 8;  // float4 loads in flight per thread
-      for (int base = 0; base < n4; base += U * kUttThreads) {
-        float4 x[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const v4i_t d = __builtin_amdgcn_raw_buffer_load_b128(
-              ro, 16 * (base + u * kUttThreads + tid), 0, kSC1);
-          x[u] = make_float4(__int_as_float(d.x), __int_as_float(d.y), __int_as_float(d.z),
-                             __int_as_float(d.w));
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int i = base + u * kUttThreads + tid;
-          if (i < n4) {
-            x[u].x *= scale; x[u].y *= scale; x[u].z *= scale; x[u].w *= scale;
-            o4[i] = x[u];
-          }
-        }
-      }
+      // the previous one's slices left over (an utterance of < 8 steps)
+      if (rs_out != nullptr) rescale_rest(std::integral_constant<int, 2 * RS_U>{});
+      rs_out = outb;
+      rs_scale = 1.0f / (pk + A.norm_eps);
+      rs_n4 = (T - 1) * H / 4;
+      rs_done = 0;
     }
     __syncthreads();  // red[] of the next utterance
     b = nb;
   }
+  // the block's last utterance, after the loop where the sample registers are dead: every
+  // load of a 4-s utterance in flight at once (the single-utterance blocks of B <= #CU
+  // rescale here; a latency-bound loop with 8 loads in flight per thread ran ~13 us)
+  if (rs_out != nullptr) rescale_rest(std::integral_constant<int, RS_BULK>{});
 }
 
 // ================================ finalize ================================
@@ -1699,11 +1756,13 @@ extern "C" int avz_debug_set_synth_variant(int v) {
 // The per-utterance kernel covers the IBM-target and unfiltered post-filters (the headline
 // and the IPD configuration); the IRM and external-mask gains, read per (bin, frame) from
 // memory, need registers it does not have (48-56 B of scratch), so those plans keep the
-// chunk grid + finalize.
+// chunk grid + finalize. It pays for peak normalisation only (the rescale folded in, no
+// finalize launch); without it the chunk grid's synthesis + seam pass is the faster pair
+// (B = 256: 70.7 + 4.2 vs 79.9 us, profiles/r04/ab_synth_utt.txt).
 template <int N, int PF, bool SPEC>
-static bool synth_per_utterance() {
+static bool synth_per_utterance(const ChainArgs* a) {
   return N == 1024 && !SPEC && (PF == PF_IBM_TARGET || PF == PF_NONE) &&
-         g_synth_variant.load(std::memory_order_relaxed) == 1;
+         a->normalize == NORM_PEAK && g_synth_variant.load(std::memory_order_relaxed) == 1;
 }
 
 // Synthesis + output normalisation of the chain and of the stage exports: the per-utterance
@@ -1714,7 +1773,7 @@ static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, h
 template <int N, int PF, bool SPEC = false>
 static int launch_synth_finalize(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1,
                                  hipEvent_t e2, hipEvent_t e3) {
-  if (synth_per_utterance<N, PF, SPEC>()) {
+  if (synth_per_utterance<N, PF, SPEC>(a)) {
     constexpr int lds = UttGeo::LDS_BYTES;
     constexpr int UPF = (PF == PF_IBM_TARGET || PF == PF_NONE) ? PF : PF_NONE;  // instantiated
     if (!lds_ready<avz_synthesis_utt_kernel<UPF>>(lds)) return -3;

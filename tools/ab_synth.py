@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--calls", type=int, default=30)
     ap.add_argument("--workload", default="ibm")
     ap.add_argument("--variants", default="0,1")
+    ap.add_argument("--normalize", default="peak")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, S = a.batch, 64000
@@ -37,11 +38,11 @@ def main():
                                             rng="philox")
     if a.workload == "ibm":
         plan = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
-                            normalize="peak", max_batch=B, max_samples=S)
+                            normalize=a.normalize, max_batch=B, max_samples=S)
         refs = dict(ref_tgt=tgt, ref_int=itf)
     else:
         plan = avz.MVDRPlan(n_fft=1024, sigma=1e-7, mic_d=0.01, mask="ipd", postfilter="none",
-                            normalize="peak", norm_eps=1e-6, max_batch=B, max_samples=S)
+                            normalize=a.normalize, norm_eps=1e-6, max_batch=B, max_samples=S)
         refs = {}
     lens = torch.full((B,), S, dtype=torch.int32, device=dev)
     out = plan.alloc_out(B, S, dev)
