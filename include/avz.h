@@ -214,7 +214,8 @@ int avz_istft(const avz_plan* plan, int batch, int frames, const float* S, long 
  * finalize), 2 = the analysis kernel only, 0 = off; enabling also resets the sums.
  * avz_plan_get_timing waits for the outstanding calls and returns the average
  * milliseconds per kernel over the calls recorded since enabling (NaN for kernels not
- * timed). Not thread-safe. */
+ * timed; finalize counts 0 in calls whose synthesis kernel folded it in — N = 1024 with
+ * peak normalisation and the IBM or no post-filter). Not thread-safe. */
 int avz_plan_set_timing(avz_plan* plan, int enable);
 /* Time one avz_mvdr_batch call in `period` (>= 1; default 1): the calls in between carry no
  * events, so a sampled timing run costs the other calls nothing. */

@@ -37,9 +37,6 @@ namespace avz {
 // stage-1 stores, ...) are recorded in DESIGN.md §6 and kept under tools/experiments/;
 // this file holds only the shipped paths.
 
-#ifndef AVZ_REF_HALF
-#define AVZ_REF_HALF 0
-#endif
 constexpr int kChunk = 32;      // frames per chunk = bits of one mask word
 constexpr int kSC1 = 16;        // buffer-op cache policy bit: sc1 (L1-bypassing loads, gfx940+)
 typedef int v4i_t __attribute__((ext_vector_type(4)));
@@ -177,10 +174,13 @@ __device__ __forceinline__ void window_fft_reg(cf (&v)[32], const WinCoef<1024>&
 
 // Reference pair of the IBM mask (N = 1024, register twiddles): the reference spectrum is
 // only needed for one bit per bin, noise <=> Re(Zr[k] Zr[N - k]) < 0 (ibm_noise). Lane l
-// holds Zr[l + 32 k]; all 32 outputs are stored as formed (so every register takes its
-// next-step load during the stage), then the lane reads back bins l + 32 k, k < 16, with
-// their partners N - (l + 32 k) and publishes their 16 bits as word l of the slot (bytes
-// 0..127). The Nyquist bin (lane 0, k = 16) stays readable at spec[N / 2].
+// holds Zr[l + 32 k]. Only the upper-half outputs (k >= 16) are stored, as formed, their
+// registers taking their next-step loads during the stage; the lower half stays in
+// registers, the lane reads the partners N - (l + 32 k), k < 16, back (all in the stored
+// upper half but DC's, which is its own partner), publishes the 16 bits as word l of the
+// slot (bytes 0..127) and only then reloads registers 0-15 (analysis 80.7-80.9 -> 79.1-79.5
+// us against storing all 32 and reading both operands back, profiles/r04/ab_ref_half.txt).
+// The Nyquist bin (lane 0, k = 16) stays readable at spec[N / 2].
 template <class After = NoAfter>
 __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCoef<1024>& wc,
                                                         const Fft1024x2& fft, cf* spec,
@@ -192,9 +192,6 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
   const int l = lm.out0;
   fft.stage1_reg_st(v, spec, tw_reg);
   fft.transpose_read(v, spec);
-#if AVZ_REF_HALF
-  // experiment: only the upper-half outputs stored (their registers reload during the
-  // stage), the lower half kept for the bits and reloaded after them
   fft.stage2_emit(v, [&](auto k, cf x) {
     if constexpr (decltype(k)::value >= 16) {
       spec[l + 32 * k] = x;
@@ -211,22 +208,6 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
   });
   reinterpret_cast<uint32_t*>(spec)[l] = w;
   static_for<0, 16>([&](auto k) { after(k); });
-#else
-  fft.stage2_emit(v, [&](auto k, cf x) {
-    spec[l + 32 * k] = x;
-    after(k);
-  });
-  __builtin_amdgcn_wave_barrier();
-  uint32_t w = 0u;
-  cf zo[16], zp[16];
-  static_for<0, 16>([&](auto k) {
-    const int m = l + 32 * k;
-    zo[k] = spec[m];
-    zp[k] = spec[(N - m) & (N - 1)];
-  });
-  static_for<0, 16>([&](auto k) { w |= (ibm_noise(zo[k], zp[k]) ? 1u : 0u) << k; });
-  reinterpret_cast<uint32_t*>(spec)[l] = w;
-#endif
 }
 
 // Window + forward FFT of the synthesis kernel and of the N = 512 analysis kernel:
@@ -1780,8 +1761,8 @@ static int launch_synth_finalize(const ChainArgs* a, hipStream_t st, hipEvent_t 
     const dim3 grid((unsigned)std::min(a->batch, resident_cus()));
     hipExtLaunchKernelGGL((avz_synthesis_utt_kernel<UPF>), grid, dim3(kUttThreads), lds, st, e0,
                           e1, 0, *a);
-    if (e2 && (hipEventRecord(e2, st) != hipSuccess || hipEventRecord(e3, st) != hipSuccess))
-      return -3;
+    (void)e2;  // no finalize launch: its events stay unrecorded (avz_chain_launches_finalize)
+    (void)e3;
     return 0;
   }
   if (launch_synthesis<N, PF, SPEC>(a, st, e0, e1) != 0) return -3;
@@ -1890,6 +1871,15 @@ extern "C" int avz_launch_srp(int n_fft, const ChainArgs* a, const SrpArgs* s, v
   if (n_fft == 1024) return launch_srp_t<1024>(a, s, (hipStream_t)stream);
   if (n_fft == 512) return launch_srp_t<512>(a, s, (hipStream_t)stream);
   return -4;
+}
+
+extern "C" int avz_chain_launches_finalize(int n_fft, const ChainArgs* a) {
+  if (n_fft != 1024) return 1;
+  switch (a->postfilter) {
+    case PF_IBM_TARGET: return synth_per_utterance<1024, PF_IBM_TARGET, false>(a) ? 0 : 1;
+    case PF_NONE: return synth_per_utterance<1024, PF_NONE, false>(a) ? 0 : 1;
+    default: return 1;
+  }
 }
 
 extern "C" int avz_launch_chunked(int n_fft, int mask_mode, const ChainArgs* a, void* stream) {

@@ -3,3 +3,4 @@ out=gpurun_out/r04j; mkdir -p $out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $out/tests_default.log 2>&1 || { tail -30 $out/tests_default.log; exit 1; }
 tail -3 $out/tests_default.log
 REPS=2 bash tools/gpu_bench_ab.sh r04j 0 1
+STAMP_ARGS="--mask ipd --batch 256" bash tools/stamps.sh r04j_ipd 0
