@@ -19,8 +19,11 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"analysis": "avz_analysis_kernel", "solve": "avz_solve_kernel",
-           "synthesis": "avz_synthesis_kernel", "finalize": "avz_finalize_kernel"}
+# the per-utterance synthesis kernel (peak normalisation at N = 1024) folds finalize in:
+# then no finalize dispatch exists and its traffic counts 0
+KERNELS = {"analysis": ("avz_analysis_kernel",), "solve": ("avz_solve_kernel",),
+           "synthesis": ("avz_synthesis_kernel", "avz_synthesis_utt_kernel"),
+           "finalize": ("avz_finalize_kernel",)}
 B, S, N = 256, 64000, 1024
 
 
@@ -31,11 +34,11 @@ def per_dispatch(path, counter):
             if row.get("Counter_Name") != counter:
                 continue
             name = row.get("Kernel_Name", "")
-            for k, pat in KERNELS.items():
-                if pat in name:
+            for k, pats in KERNELS.items():
+                if any(p in name for p in pats):
                     d = int(row["Dispatch_Id"])
                     vals[k][d] = vals[k].get(d, 0.0) + float(row["Counter_Value"])
-    return {k: (sum(v.values()) / len(v) if v else None) for k, v in vals.items()}
+    return {k: (sum(v.values()) / len(v) if v else 0.0) for k, v in vals.items()}
 
 
 def main():
