@@ -162,8 +162,9 @@ def _load():
     if lib.avz_version() != ABI_VERSION:  # the struct layouts above are version 2's
         raise ImportError(f"libavz ABI version {lib.avz_version()} != {ABI_VERSION} "
                           "(AvzBatchArgs / AvzSpectralArgs layouts); rebuild")
-    # diagnostic A/B of the synthesis paths (tools/ab_synth.py, bench.py runs): 1 the
-    # per-utterance kernel (default), 0 the chunk grid + finalize
+    # diagnostic A/B of the synthesis paths (tools/ab_synth.py, bench.py runs): 2 the
+    # per-utterance kernel solving its own bins (default), 1 the same after the solve
+    # kernel, 0 the chunk grid + finalize
     if os.environ.get("AVZ_SYNTH_VARIANT") and hasattr(lib, "avz_debug_set_synth_variant"):
         lib.avz_debug_set_synth_variant(int(os.environ["AVZ_SYNTH_VARIANT"]))
     return lib

@@ -69,7 +69,7 @@ struct avz_plan {
   // (hipExtLaunchKernel): no marker packets between the chain's launches
   hipEvent_t ev[2][8];
   bool ev_pending[2];
-  bool ev_fin[2];  // the set's call launched the finalize kernel (else its events are unused)
+  int ev_kern[2];  // kernels the set's call launched (avz_chain_kernels bits; others count 0)
   int ev_next;
   int period;      // events on one avz_mvdr_batch call in `period` (avz_plan_set_timing_period)
   long long seen;  // calls since timing was enabled
@@ -80,9 +80,12 @@ struct avz_plan {
 static void timing_drain(avz_plan* p, int set) {
   if (!p->ev_pending[set]) return;
   p->ev_pending[set] = false;
-  const int n_k = (p->n_k == 4 && !p->ev_fin[set]) ? 3 : p->n_k;  // finalize counts 0
-  if (hipEventSynchronize(p->ev[set][2 * n_k - 1]) != hipSuccess) return;
-  for (int i = 0; i < n_k; ++i) {
+  int last = 0;  // the last launched kernel's stop event
+  for (int i = 0; i < p->n_k; ++i)
+    if ((p->ev_kern[set] >> i) & 1) last = i;
+  if (hipEventSynchronize(p->ev[set][2 * last + 1]) != hipSuccess) return;
+  for (int i = 0; i < p->n_k; ++i) {
+    if (!((p->ev_kern[set] >> i) & 1)) continue;  // folded into another kernel: 0 ms
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, p->ev[set][2 * i], p->ev[set][2 * i + 1]) == hipSuccess)
       p->ms_sum[i] += ms;
@@ -354,7 +357,7 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
   const int rc = hip_rc(avz_launch_chunked(p->cfg.n_fft, p->cfg.mask_mode, &k, stream));
   if (set >= 0 && rc == AVZ_OK) {
     mp->ev_pending[set] = true;
-    mp->ev_fin[set] = avz_chain_launches_finalize(p->cfg.n_fft, &k) != 0;
+    mp->ev_kern[set] = avz_chain_kernels(p->cfg.n_fft, &k);
   }
   return rc;
 }

@@ -755,6 +755,48 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysi
 // cov/w debug outputs).
 constexpr int kSolveThreads = 256;
 
+// Covariance sums of bin k of utterance b: fp64 sum of its nch chunk partials, scaled back
+// by 1/4 (the analysis accumulates (2 y)(2 y)^H).
+template <int N>
+__device__ __forceinline__ void bin_cov_sums(const ChainArgs& A, int b, int k, int nch,
+                                             double (&R)[5]) {
+  constexpr int F = N / 2 + 1;
+  const float* P = A.part + (long long)b * A.nchunk * 5 * F + k;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) R[q] = 0.0;
+  for (int cc = 0; cc < nch; ++cc) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) R[q] += (double)P[((long long)cc * 5 + q) * F];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) R[q] *= 0.25;
+}
+// The same for a block-uniform utterance b (the per-utterance synthesis kernel): the
+// partials of up to four chunks per round trip through a buffer descriptor covering
+// exactly the utterance's nch chunks, so the loads of absent chunks read +0 without
+// branches and the sums (chunk order kept, + 0 changes nothing) are bitwise those above.
+template <int N>
+__device__ __forceinline__ void bin_cov_sums_utt(const ChainArgs& A, int b, int k, int nch,
+                                                 double (&R)[5]) {
+  constexpr int F = N / 2 + 1;
+  const rsrc_t rp = make_rsrc(A.part + (long long)b * A.nchunk * 5 * F, (long long)nch * 5 * F);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) R[q] = 0.0;
+  for (int c0 = 0; c0 < nch; c0 += 4) {
+    float p[4][5];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) p[i][q] = bload_nn(rp, ((c0 + i) * 5 + q) * F + k);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) R[q] += (double)p[i][q];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) R[q] *= 0.25;
+}
+
 template <int N>
 __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   constexpr int H = N / 2, F = N / 2 + 1;
@@ -765,14 +807,8 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   if (L < N) return;
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
-  const float* P = A.part + (long long)b * A.nchunk * 5 * F + k;
-  double R[5] = {0, 0, 0, 0, 0};
-  for (int cc = 0; cc < nch; ++cc) {
-#pragma unroll
-    for (int q = 0; q < 5; ++q) R[q] += (double)P[((long long)cc * 5 + q) * F];
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) R[q] *= 0.25;  // analysis accumulates (2 y)(2 y)^H
+  double R[5];
+  bin_cov_sums<N>(A, b, k, nch, R);
   if (A.cov_only) {  // covariance stage export
 #pragma unroll
     for (int q = 0; q < 5; ++q) A.cov_out[((long long)b * F + k) * 5 + q] = R[q];
@@ -1253,9 +1289,6 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_syn
 // wave's own spectra); the block meets twice per step, around the overlap-add of the 16
 // segments, which reads neighbouring waves' frames. Reference semantics as the two-block
 // kernel + avz_finalize_kernel (oracle_debug.py:80-94, scipy istft's OLA and N/2 trim).
-#ifndef AVZ_UTT_LOADS
-#define AVZ_UTT_LOADS 2
-#endif
 constexpr int kUttThreads = 512;
 struct UttGeo {
   static constexpr int N = 1024, H = 512, F = 513, FB = 16;  // frames per step: 8 waves x 2
@@ -1271,7 +1304,11 @@ __device__ __forceinline__ cf* utt_frame(unsigned char* lds, int f) {
   return reinterpret_cast<cf*>(lds + f * UttGeo::SLOT);
 }
 
-template <int PF>
+// SOLVE: the block solves its utterance's 513 bins itself (the MVDR solve of
+// avz_solve_kernel, one bin per thread, straight into the LDS coefficient table) instead of
+// reading the solve kernel's coef[] -- no solve launch (plain MVDR plans without the
+// item-level fallback or debug outputs).
+template <int PF, bool SOLVE>
 __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(ChainArgs A) {
   constexpr int N = UttGeo::N, H = UttGeo::H, F = UttGeo::F, FB = UttGeo::FB;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -1402,9 +1439,22 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     // the utterance's apply coefficients into LDS (read per step, so they hold no registers
     // through the FFTs); the previous utterance's readers finished at its last barrier
     {
-      const float4* coef = reinterpret_cast<const float4*>(A.coef) + (long long)b * F;
       float4* ct = reinterpret_cast<float4*>(lds + UttGeo::COEF_OFF);
-      for (int k = tid; k < F; k += kUttThreads) ct[k] = coef[k];
+      if constexpr (SOLVE) {
+        const int nch = (T + kChunk - 1) / kChunk;
+        for (int k = tid; k < F; k += kUttThreads) {
+          double R[5], w[4];
+          bin_cov_sums_utt<N>(A, b, k, nch, R);
+          const double* d = A.steer + 4 * k;
+          mvdr_weights_d(R, k, N, A, d[0], d[1], d[2], d[3], w, nullptr);
+          cf al, be;
+          coef_from_w(w[0], w[1], w[2], w[3], al, be, nullptr);
+          ct[k] = make_float4(al.x, al.y, be.x, be.y);
+        }
+      } else {
+        const float4* coef = reinterpret_cast<const float4*>(A.coef) + (long long)b * F;
+        for (int k = tid; k < F; k += kUttThreads) ct[k] = coef[k];
+      }
     }
     __syncthreads();
     uint32_t bits[9];
@@ -1431,8 +1481,8 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       const rsrc_t q0 = more ? r0 : (wave >= 1 ? n0 : r_none);
       const rsrc_t q1 = more ? r1 : (wave >= 1 ? n1 : r_none);
       const int sn = ((more ? f0 + FB : 0) + my) * H - N / 2 + lm.in0;
-      // AVZ_UTT_LOADS (experiment): where the next step's loads are issued -- 0 from inside
-      // the forward FFT's last stage, 1 after the FFT, 2 after the apply, 3 after the inverse
+      // the next step's loads go out after the apply (issued from inside the forward FFT's
+      // last stage, after the FFT or after the inverse measured slower)
       auto next_loads = [&]() {
         if (il) {
           static_for<0, 32>([&](auto k) {
@@ -1443,17 +1493,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
           first_loads(n0, n1);  // wave 0, last step: the next utterance (or empty)
         }
       };
-      if constexpr (AVZ_UTT_LOADS == 0) {
-        window_fft<N>(v, wc0, fft, utt_frame(lds, my), lm, [&](auto kc) {
-          constexpr int k = decltype(kc)::value;
-          v[k].x = bload_nn(q0, sn + 32 * k);
-          v[k].y = bload_nn(q1, sn + 32 * k);
-        });
-        if (!il) first_loads(n0, n1);
-      } else {
-        window_fft<N>(v, wc0, fft, utt_frame(lds, my), lm);
-        if (AVZ_UTT_LOADS == 1) next_loads();
-      }
+      window_fft<N>(v, wc0, fft, utt_frame(lds, my), lm);
       __builtin_amdgcn_wave_barrier();
       const float* irm = (PF == PF_IRM) ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F
                                         : nullptr;
@@ -1518,7 +1558,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
           Z[N / 4] = {2.0f * s.x, -2.0f * s.y};
         }
       }
-      if (AVZ_UTT_LOADS == 2) next_loads();
+      next_loads();
       __builtin_amdgcn_wave_barrier();
       // ---- inverse: lane group g transforms frame 2 wave + g; windowed contributions
       // (samples 2m, 2m + 1 as one float2) over the frame's first 4 KB, the transpose in its
@@ -1536,7 +1576,6 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
           Cp[mhs + 16 * k] = make_float2(x.x * we, -x.y * wo);
         });
       }
-      if (AVZ_UTT_LOADS == 3) next_loads();
       lds_barrier();
       // ---- overlap-add: segment j = f0 - 1 + s = frame s-1 (2nd half) + frame s (1st half);
       // segment -1 (frame 0's first half) is scipy's trimmed N/2
@@ -1728,9 +1767,9 @@ static int resident_cus();
 // Synthesis kernel selection (diagnostic A/B, avz_debug_set_synth_variant): 1 = the
 // per-utterance kernel for N = 1024 time-domain input (no finalize launch), 0 = the
 // two-block chunk kernel + avz_finalize_kernel.
-static std::atomic<int> g_synth_variant{1};
+static std::atomic<int> g_synth_variant{2};
 extern "C" int avz_debug_set_synth_variant(int v) {
-  if (v < 0 || v > 1) return -1;
+  if (v < 0 || v > 2) return -1;
   g_synth_variant.store(v);
   return 0;
 }
@@ -1743,7 +1782,15 @@ extern "C" int avz_debug_set_synth_variant(int v) {
 template <int N, int PF, bool SPEC>
 static bool synth_per_utterance(const ChainArgs* a) {
   return N == 1024 && !SPEC && (PF == PF_IBM_TARGET || PF == PF_NONE) &&
-         a->normalize == NORM_PEAK && g_synth_variant.load(std::memory_order_relaxed) == 1;
+         a->normalize == NORM_PEAK && g_synth_variant.load(std::memory_order_relaxed) >= 1;
+}
+// ... and solves the utterance's bins itself (variant 2) when the chain's solve is the plain
+// MVDR one: no item-level fallback flags, no covariance / weight debug outputs.
+template <int N, int PF>
+static bool solve_fused(const ChainArgs* a) {
+  return synth_per_utterance<N, PF, false>(a) && g_synth_variant.load(std::memory_order_relaxed) == 2 &&
+         a->beamformer == BF_MVDR && a->singular_fallback != 2 && !a->cov_out && !a->w_out &&
+         !a->cov_only;
 }
 
 // Synthesis + output normalisation of the chain and of the stage exports: the per-utterance
@@ -1753,15 +1800,17 @@ template <int N, int PF, bool SPEC = false>
 static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
 template <int N, int PF, bool SPEC = false>
 static int launch_synth_finalize(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1,
-                                 hipEvent_t e2, hipEvent_t e3) {
+                                 hipEvent_t e2, hipEvent_t e3, bool fused_solve = false) {
   if (synth_per_utterance<N, PF, SPEC>(a)) {
     constexpr int lds = UttGeo::LDS_BYTES;
     constexpr int UPF = (PF == PF_IBM_TARGET || PF == PF_NONE) ? PF : PF_NONE;  // instantiated
-    if (!lds_ready<avz_synthesis_utt_kernel<UPF>>(lds)) return -3;
+    auto kern = fused_solve ? avz_synthesis_utt_kernel<UPF, true> : avz_synthesis_utt_kernel<UPF, false>;
+    if (!(fused_solve ? lds_ready<avz_synthesis_utt_kernel<UPF, true>>(lds)
+                      : lds_ready<avz_synthesis_utt_kernel<UPF, false>>(lds)))
+      return -3;
     const dim3 grid((unsigned)std::min(a->batch, resident_cus()));
-    hipExtLaunchKernelGGL((avz_synthesis_utt_kernel<UPF>), grid, dim3(kUttThreads), lds, st, e0,
-                          e1, 0, *a);
-    (void)e2;  // no finalize launch: its events stay unrecorded (avz_chain_launches_finalize)
+    hipExtLaunchKernelGGL(kern, grid, dim3(kUttThreads), lds, st, e0, e1, 0, *a);
+    (void)e2;  // no finalize launch: its events stay unrecorded (avz_chain_kernels)
     (void)e3;
     return 0;
   }
@@ -1826,7 +1875,9 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
   if (item_fallback && hipMemsetAsync(a->flag, 0, sizeof(int) * a->batch, st) != hipSuccess)
     return -3;
   hipExtLaunchKernelGGL(k1, pgrid, dim3(kCThreads), lds, st, evt(0), evt(1), 0, *a);
-  if (item_fallback) {
+  const bool fused = solve_fused<N, PF>(a);  // the synthesis kernel solves (no launch here)
+  if (fused) {
+  } else if (item_fallback) {
     hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), nullptr, 0, *a);
     hipExtLaunchKernelGGL(avz_solve_fixup_kernel<N>, dim3(nsolve), dim3(kSolveThreads), 0, st,
                           nullptr, evt(3), 0, *a);
@@ -1834,7 +1885,7 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
     hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), evt(3), 0, *a);
   }
   (void)k3;
-  if (launch_synth_finalize<N, PF>(a, st, evt(4), evt(5), evt(6), evt(7)) != 0) return -3;
+  if (launch_synth_finalize<N, PF>(a, st, evt(4), evt(5), evt(6), evt(7), fused) != 0) return -3;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -1873,13 +1924,16 @@ extern "C" int avz_launch_srp(int n_fft, const ChainArgs* a, const SrpArgs* s, v
   return -4;
 }
 
-extern "C" int avz_chain_launches_finalize(int n_fft, const ChainArgs* a) {
-  if (n_fft != 1024) return 1;
-  switch (a->postfilter) {
-    case PF_IBM_TARGET: return synth_per_utterance<1024, PF_IBM_TARGET, false>(a) ? 0 : 1;
-    case PF_NONE: return synth_per_utterance<1024, PF_NONE, false>(a) ? 0 : 1;
-    default: return 1;
+extern "C" int avz_chain_kernels(int n_fft, const ChainArgs* a) {
+  bool utt = false, fused = false;
+  if (n_fft == 1024 && a->postfilter == PF_IBM_TARGET) {
+    utt = synth_per_utterance<1024, PF_IBM_TARGET, false>(a);
+    fused = solve_fused<1024, PF_IBM_TARGET>(a);
+  } else if (n_fft == 1024 && a->postfilter == PF_NONE) {
+    utt = synth_per_utterance<1024, PF_NONE, false>(a);
+    fused = solve_fused<1024, PF_NONE>(a);
   }
+  return 1 | (fused ? 0 : 2) | 4 | (utt ? 0 : 8);
 }
 
 extern "C" int avz_launch_chunked(int n_fft, int mask_mode, const ChainArgs* a, void* stream) {

@@ -163,9 +163,11 @@ int avz_launch_chunk_split(const avz::ChunkSplitArgs* a, void* stream);
 int avz_launch_metrics(const avz::MetricsArgs* a, void* stream);
 int avz_launch_chunk_merge(const avz::ChunkMergeArgs* a, void* stream);
 int avz_launch_chunked(int n_fft, int mask_mode, const avz::ChainArgs* a, void* stream);
-// 0 when avz_launch_chunked synthesises per utterance (the rescale folded in, no finalize
-// launch; its finalize events are not recorded)
-int avz_chain_launches_finalize(int n_fft, const avz::ChainArgs* a);
+// Kernels avz_launch_chunked launches for these arguments, bit i = kernel i (analysis,
+// solve, synthesis, finalize): the per-utterance synthesis folds finalize in (bit 3 clear)
+// and, for plain MVDR plans, the solve too (bit 1 clear); unlaunched kernels' events stay
+// unrecorded.
+int avz_chain_kernels(int n_fft, const avz::ChainArgs* a);
 // stage exports: analysis + partial sums -> cov_out; w [B][F][4] -> coef -> synthesis +
 // finalize (post-filter PF_NONE or PF_EXT_MUL with ext_mask as the gain); S -> synthesis
 // (spectrum input) + finalize
