@@ -1590,8 +1590,12 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         const int j = f0 - 1 + s;
         if (j >= 0 && j <= T - 2) {
           const float4 vb = *reinterpret_cast<const float4*>(cframe(s) + m0);
-          float4 va = carry;  // a select of values, not of pointers (that put carry on the stack)
-          if (s != 0) va = *reinterpret_cast<const float4*>(cframe(s - 1) + H + m0);
+          // the previous frame's half read unconditionally (frame 0's when s = 0) and the
+          // carry selected by value: a conditional read was split into four ds_read_b32
+          // (4-way bank conflicts, 15 % of the kernel's LDS cycles), a pointer select with
+          // &carry put carry on the stack
+          const float4 vp = *reinterpret_cast<const float4*>(cframe(s == 0 ? 0 : s - 1) + H + m0);
+          const float4 va = (s != 0) ? vp : carry;
           float4 o;
           o.x = (va.x + vb.x) * inv[0];
           o.y = (va.y + vb.y) * inv[1];
