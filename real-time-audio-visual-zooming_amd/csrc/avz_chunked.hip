@@ -1349,6 +1349,8 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
   for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(4 * (tid & 127) + i);
   const rsrc_t r_none = make_rsrc(nullptr, 0);
   __syncthreads();  // twiddle table
+  AVZ_STAMP_DECL();
+  AVZ_STAMP_INIT();
 
   // the block's utterances b = blockIdx.x, + gridDim.x, ...; one with a bad device length
   // (host validates) reports NaN, as finalize does, and is skipped
@@ -1457,11 +1459,16 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       }
     }
     __syncthreads();
+    AVZ_STAMP(15);
     uint32_t bits[9];
     float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);
     float peak = 0.0f;
     float* outb = A.out + (long long)b * A.out_stride;
     for (int step = 0; step < nstep; ++step) {
+#ifdef AVZ_STAMPS
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      AVZ_STAMP(13);
+#endif
       const int f0 = step * FB, c = f0 / kChunk;
       // lane-derived LDS / global offsets recomputed per step (held across the loop they
       // cost ~100 VGPRs and spilled)
@@ -1494,6 +1501,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         }
       };
       window_fft<N>(v, wc0, fft, utt_frame(lds, my), lm);
+      AVZ_STAMP(4);
       __builtin_amdgcn_wave_barrier();
       const float* irm = (PF == PF_IRM) ? A.pf_gain + ((long long)b * A.nchunk + c) * kChunk * F
                                         : nullptr;
@@ -1558,7 +1566,9 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
           Z[N / 4] = {2.0f * s.x, -2.0f * s.y};
         }
       }
+      AVZ_STAMP(5);
       next_loads();
+      AVZ_STAMP(6);
       __builtin_amdgcn_wave_barrier();
       // ---- inverse: lane group g transforms frame 2 wave + g; windowed contributions
       // (samples 2m, 2m + 1 as one float2) over the frame's first 4 KB, the transpose in its
@@ -1576,7 +1586,9 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
           Cp[mhs + 16 * k] = make_float2(x.x * we, -x.y * wo);
         });
       }
+      AVZ_STAMP(7);
       lds_barrier();
+      AVZ_STAMP(8);
       // ---- overlap-add: segment j = f0 - 1 + s = frame s-1 (2nd half) + frame s (1st half);
       // segment -1 (frame 0's first half) is scipy's trimmed N/2
       auto cframe = [&](int f) -> const float* {
@@ -1614,7 +1626,9 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         ola();
       }
       if (sgrp == 0) carry = *reinterpret_cast<const float4*>(cframe(FB - 1) + H + m0);
+      AVZ_STAMP(9);
       lds_barrier();
+      AVZ_STAMP(10);
     }
     // ---- utterance peak; NORM_PEAK rescales the block's own output (its stores drained
     // first; L1-bypassing loads), as avz_finalize_kernel did in a second pass over HBM
@@ -1635,12 +1649,14 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       rs_done = 0;
     }
     __syncthreads();  // red[] of the next utterance
+    AVZ_STAMP(14);
     b = nb;
   }
   // the block's last utterance, after the loop where the sample registers are dead: every
   // load of a 4-s utterance in flight at once (the single-utterance blocks of B <= #CU
   // rescale here; a latency-bound loop with 8 loads in flight per thread ran ~13 us)
   if (rs_out != nullptr) rescale_rest(std::integral_constant<int, RS_BULK>{});
+  AVZ_STAMP(14);
 }
 
 // ================================ finalize ================================

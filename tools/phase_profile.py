@@ -26,6 +26,10 @@ from avz import synth  # noqa: E402
 PHASES = ["A load wait", "A barrier 1", "A barrier 2", "A window+FFT", "S prologue",
           "S load wait", "S FFT", "S apply", "S iFFT", "S OLA", "S peak", "A load issue",
           "A bins", "-", "-", "-"]
+# the per-utterance synthesis kernel (avz_synthesis_utt_kernel)
+UTT_PHASES = {4: "U window+FFT", 5: "U apply", 6: "U next loads", 7: "U iFFT",
+              8: "U barrier 1", 9: "U OLA+rescale", 10: "U barrier 2", 13: "U load wait",
+              14: "U utt end", 15: "U solve"}
 RS_PHASES = {4: "P prologue", 5: "P window+FFT", 6: "P next loads", 7: "P barrier",
              8: "C apply", 9: "C iFFT", 10: "C sync wait", 13: "C OLA", 14: "C barrier",
              15: "C item coefs"}
@@ -37,9 +41,14 @@ ap.add_argument("--mask", default="ibm")
 ap.add_argument("--normalize", default="peak")
 ap.add_argument("--seconds", type=float, default=4.0)
 ap.add_argument("--synth-variant", type=int, default=-1, help="avz_debug_set_synth_variant")
+ap.add_argument("--utt", action="store_true",
+                help="label slots 4-10, 13-15 as the per-utterance synthesis kernel's phases")
 a = ap.parse_args()
-if a.synth_variant >= 0:
+if a.synth_variant >= 0 and not a.utt:
     PHASES = [RS_PHASES.get(i, n) if i >= 4 and a.synth_variant == 1 else n
+              for i, n in enumerate(PHASES)]
+if a.utt:
+    PHASES = [UTT_PHASES.get(i, n) if i >= 4 and i not in (11, 12) else n
               for i, n in enumerate(PHASES)]
 S = int(a.seconds * 16000)
 dev = torch.device("cuda:0")
