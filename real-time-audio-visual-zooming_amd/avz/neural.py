@@ -92,6 +92,28 @@ class FreqPreservingUNet(nn.Module):
         return self.out(x).squeeze(1)
 
 
+def fold_batchnorm(model: nn.Module) -> nn.Module:
+    """Inference copy of an eval-mode model with every (Conv2d, BatchNorm2d) pair of its
+    Sequential blocks folded into one Conv2d (w * g / sqrt(v + eps), (b - m) g / sqrt(v +
+    eps) + beta; torch.nn.utils.fusion.fuse_conv_bn_eval) and the BatchNorm replaced by
+    Identity: the U-Net's 14 BatchNorm launches per forward disappear. Module names are
+    unchanged; the result differs from the unfolded model by fp32 rounding only."""
+    import copy
+
+    from torch.nn.utils.fusion import fuse_conv_bn_eval
+    if model.training:
+        raise ValueError("fold_batchnorm needs an eval-mode model")
+    m = copy.deepcopy(model)
+    for seq in m.modules():
+        if not isinstance(seq, nn.Sequential):
+            continue
+        for i in range(len(seq) - 1):
+            if isinstance(seq[i], nn.Conv2d) and isinstance(seq[i + 1], nn.BatchNorm2d):
+                seq[i] = fuse_conv_bn_eval(seq[i], seq[i + 1])
+                seq[i + 1] = nn.Identity()
+    return m
+
+
 class NeuralMaskBeamformer:
     """Batched main_deploy core: [B, 2, S] device mixtures -> [B, S] enhanced signals.
 
@@ -100,11 +122,16 @@ class NeuralMaskBeamformer:
     ``model_dtype``: torch.float32 (reference precision) or torch.bfloat16 (the forward
     runs in bf16, the mask is handed to the HIP chain in fp32). ``channels_last``: NHWC
     activations for the convolutions (fp32 results equal to within 1e-7 of NCHW on MI355X,
-    ~3 % faster forward; tools/unet_speed.py)."""
+    ~3 % faster forward; tools/unet_speed.py). ``fold_bn``: an eval-mode model runs as its
+    BatchNorm-folded copy (fold_batchnorm)."""
 
     def __init__(self, model: nn.Module, max_items: int, conf: dict | None = None,
-                 model_batch: int = 256, model_dtype=torch.float32, channels_last: bool = True):
+                 model_batch: int = 256, model_dtype=torch.float32, channels_last: bool = True,
+                 fold_bn: bool = True):
         conf = conf or CONF
+        if fold_bn and not model.training and any(
+                isinstance(x, nn.BatchNorm2d) for x in model.modules()):
+            model = fold_batchnorm(model)
         self.channels_last = channels_last
         if channels_last:
             model = model.to(memory_format=torch.channels_last)

@@ -42,6 +42,33 @@ def test_unet_forward_matches_reference_mask(unet):
     np.testing.assert_allclose(m, g["masks"][0], atol=1e-6)
 
 
+def test_batchnorm_folded_unet_matches_reference_mask(unet):
+    """fold_batchnorm (the inference copy NeuralMaskBeamformer runs): no BatchNorm left,
+    the original model untouched, and the same reference mask within fp32 rounding —
+    with the reference's fresh BN statistics and with non-trivial ones."""
+    from avz.neural import fold_batchnorm
+    model, g = unet
+    folded = fold_batchnorm(model)
+    assert not any(isinstance(m, torch.nn.BatchNorm2d) for m in folded.modules())
+    assert any(isinstance(m, torch.nn.BatchNorm2d) for m in model.modules())
+    x = torch.from_numpy(g["feat0"])[None]
+    with torch.no_grad():
+        np.testing.assert_allclose(folded(x).numpy()[0], g["masks"][0], atol=1e-6)
+    import copy
+    m2 = copy.deepcopy(model)
+    gen = torch.Generator().manual_seed(3)
+    for bn in (m for m in m2.modules() if isinstance(m, torch.nn.BatchNorm2d)):
+        bn.running_mean.copy_(torch.rand(bn.num_features, generator=gen) - 0.5)
+        bn.running_var.copy_(torch.rand(bn.num_features, generator=gen) + 0.5)
+        bn.weight.data.copy_(torch.rand(bn.num_features, generator=gen) + 0.5)
+        bn.bias.data.copy_(torch.rand(bn.num_features, generator=gen) - 0.5)
+    with torch.no_grad():
+        a, b = m2(x), fold_batchnorm(m2)(x)
+    assert float((a - b).abs().max()) <= 1e-6
+    with pytest.raises(ValueError):
+        fold_batchnorm(copy.deepcopy(model).train())
+
+
 def test_unet_features_oracle(unet):
     _, g = unet
     mix, _, _ = triple_f32("test", g["seg"])
