@@ -1659,6 +1659,325 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
   AVZ_STAMP(14);
 }
 
+// ======================= per-utterance synthesis (N = 512) =======================
+// The N = 512 form of avz_synthesis_utt_kernel: one 8-wave block per CU owns whole
+// utterances and normalises them itself, but keeps the chunk kernel's step (synthesis_item
+// at N = 512): every lane group transforms two frames (R = 2), so a step is 32 frames -- one
+// IBM mask chunk -- in 32 slots of 4.3 KB (139 KB), and the 16 packed inverse pairs
+// (Sa + i Sb, one complex Fft512x2 per lane group) keep all eight waves busy through the
+// inverse (at N = 1024 the same packing would leave half the waves idle, hence that
+// kernel's per-frame half-size inverse). Apply: thread t serves bin t & 255 for the frame
+// pairs 8 (t >> 8) .. + 8. Seam carried in registers across the chunks, peak and rescale
+// in-block (progressive over the next utterance's overlap-add phases), solve in-block
+// (SOLVE), as the N = 1024 kernel. Reference semantics as the chunk kernel + finalize.
+constexpr int kUtt512Threads = 512;
+struct Utt512Geo {
+  static constexpr int N = 512, H = 256, F = 257, NWAVE = 8, FPW = 2, R = 2;
+  static constexpr int RSTRIDE = NWAVE * FPW;       // 16: a lane group's second frame
+  static constexpr int FB = RSTRIDE * R;            // 32 frames per step
+  static constexpr int NPAIR = FB / 2;              // 16 packed inverse pairs
+  static constexpr int SLOT_LDS = FB * KCfg<512>::GROUP_BYTES;
+  static constexpr int COEF_OFF = SLOT_LDS;         // the utterance's alpha, beta
+  static constexpr int RED_OFF = COEF_OFF + F * 16;
+  static constexpr int LDS_BYTES = RED_OFF + 64;
+  static_assert(FB == kChunk, "a step is one mask chunk");
+  static_assert(LDS_BYTES <= 160 * 1024, "one block per CU");
+  static_assert(KCfg<512>::WAVE_BYTES == FPW * KCfg<512>::GROUP_BYTES, "slot_ptr layout");
+};
+
+template <int PF, bool SOLVE>
+__global__ void __launch_bounds__(kUtt512Threads, 2) avz_synthesis_utt512_kernel(ChainArgs A) {
+  using G = Utt512Geo;
+  using C = KCfg<512>;
+  constexpr int N = G::N, H = G::H, F = G::F, FB = G::FB, NPAIR = G::NPAIR, RSTRIDE = G::RSTRIDE;
+  constexpr int PPL = C::PPL;
+  constexpr int M4 = H / 4;                    // float4 groups per half frame
+  constexpr int NSG = kUtt512Threads / M4;     // 8 segment groups (one per wave)
+  constexpr int SPT = FB / NSG;                // 4 segments per thread per step
+  constexpr int PPT = NPAIR / 2;               // 8 frame pairs per apply thread
+  extern __shared__ __align__(16) unsigned char lds[];
+  float* red = reinterpret_cast<float*>(lds + G::RED_OFF);
+  float4* ct = reinterpret_cast<float4*>(lds + G::COEF_OFF);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  Fft512x2 fft;
+  fft.init(lane);
+  LaneMap<N> lm;
+  lm.init(lane);
+  const WinCoef<N> wc = [&] { WinCoef<N> w; w.init(lm); return w; }();
+  const int my_slot = wave * G::FPW + lm.grp;  // frames my_slot, my_slot + 16 of the step
+  const int p0 = PPT * (wave >> 2);  // apply: pairs p0 .. p0 + 7 (wave-uniform)
+  const bool nyq_wave = (wave == G::NWAVE - 1);
+  const int sgrp = wave;             // overlap-add: segments wave + 8 si
+  static_assert(M4 == 64, "one segment group per wave");
+  float inv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(4 * lane + i);
+  const rsrc_t r_none = make_rsrc(nullptr, 0);
+  AVZ_STAMP_DECL();
+  AVZ_STAMP_INIT();
+
+  auto next_valid = [&](int bb) {
+    for (; bb < A.batch; bb += gridDim.x) {
+      if (utt_len(A, bb) >= N) break;
+      if (tid == 0 && A.peak) A.peak[bb] = __builtin_nanf("");
+    }
+    return bb;
+  };
+  auto rsrcs = [&](int bb, rsrc_t& a0, rsrc_t& a1) {
+    const float* mixb = A.mix + (long long)bb * A.mix_stride;
+    const int len = utt_len(A, bb);
+    a0 = make_rsrc(mixb, len);
+    a1 = make_rsrc(mixb + A.ch_stride, len);
+  };
+  cf v[PPL], vq[PPL];
+  // frames fb + my_slot (v) and fb + my_slot + 16 (vq); a step's first wave starts N/2 before
+  // sample 0 only at fb = 0 on wave 0 (range-checked offsets there)
+  auto load_step = [&](rsrc_t a0, rsrc_t a1, int fb) {
+    const int s0 = (fb + my_slot) * H - N / 2 + lm.in0, s1 = s0 + RSTRIDE * H;
+    if (fb + wave * G::FPW >= 1) {
+      static_for<0, PPL>([&](auto r) {
+        v[r].x = bload_nn(a0, s0 + C::IN_STRIDE * r);
+        v[r].y = bload_nn(a1, s0 + C::IN_STRIDE * r);
+      });
+    } else {
+      static_for<0, PPL>([&](auto r) {
+        v[r].x = bload(a0, s0 + C::IN_STRIDE * r);
+        v[r].y = bload(a1, s0 + C::IN_STRIDE * r);
+      });
+    }
+    static_for<0, PPL>([&](auto r) {
+      vq[r].x = bload_nn(a0, s1 + C::IN_STRIDE * r);
+      vq[r].y = bload_nn(a1, s1 + C::IN_STRIDE * r);
+    });
+  };
+  int b = next_valid(blockIdx.x);
+  if (b < A.batch) {
+    rsrc_t a0, a1;
+    rsrcs(b, a0, a1);
+    load_step(a0, a1, 0);
+  }
+  // NORM_PEAK rescale of the block's previous utterance, one slice per overlap-add phase
+  float* rs_out = nullptr;
+  float rs_scale = 0.0f;
+  int rs_n4 = 0, rs_done = 0;
+  constexpr int RS_U = 4, RS_BULK = 32;
+  auto rescale_slice = [&](auto uc, int lo, int hi, auto issue_more) {
+    constexpr int U = decltype(uc)::value;
+    const rsrc_t ro = make_rsrc(rs_out, 4LL * rs_n4);
+    float4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const v4i_t d = __builtin_amdgcn_raw_buffer_load_b128(ro, 16 * (lo + u * kUtt512Threads + tid),
+                                                            0, kSC1);
+      x[u] = make_float4(__int_as_float(d.x), __int_as_float(d.y), __int_as_float(d.z),
+                         __int_as_float(d.w));
+    }
+    issue_more();
+    float4* o4 = reinterpret_cast<float4*>(rs_out);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = lo + u * kUtt512Threads + tid;
+      if (i < hi) {
+        x[u].x *= rs_scale; x[u].y *= rs_scale; x[u].z *= rs_scale; x[u].w *= rs_scale;
+        o4[i] = x[u];
+      }
+    }
+  };
+  auto rescale_rest = [&](auto uc) {
+    constexpr int U = decltype(uc)::value;
+    for (; rs_done < rs_n4; rs_done += U * kUtt512Threads)
+      rescale_slice(uc, rs_done, min(rs_n4, rs_done + U * kUtt512Threads), [] {});
+    rs_out = nullptr;
+  };
+
+  while (b < A.batch) {
+    const int L = utt_len(A, b);
+    const int T = (L + H - 1) / H + 1;
+    const int nstep = (T + FB - 1) / FB;
+    rsrc_t r0, r1;
+    rsrcs(b, r0, r1);
+    const int nb = next_valid(b + gridDim.x);
+    rsrc_t n0 = r_none, n1 = r_none;
+    if (nb < A.batch) rsrcs(nb, n0, n1);
+    if constexpr (SOLVE) {
+      const int nch = (T + kChunk - 1) / kChunk;
+      for (int k = tid; k < F; k += kUtt512Threads) {
+        double R[5], w[4];
+        bin_cov_sums_utt<N>(A, b, k, nch, R);
+        const double* d = A.steer + 4 * k;
+        mvdr_weights_d(R, k, N, A, d[0], d[1], d[2], d[3], w, nullptr);
+        cf al, be;
+        coef_from_w(w[0], w[1], w[2], w[3], al, be, nullptr);
+        ct[k] = make_float4(al.x, al.y, be.x, be.y);
+      }
+    } else {
+      const float4* coef = reinterpret_cast<const float4*>(A.coef) + (long long)b * F;
+      for (int k = tid; k < F; k += kUtt512Threads) ct[k] = coef[k];
+    }
+    __syncthreads();
+    AVZ_STAMP(15);
+    cf alpha, beta, alpha_n{0, 0}, beta_n{0, 0};
+    {
+      const float4 w = ct[tid & 255];
+      alpha = cf{w.x, w.y};
+      beta = cf{w.z, w.w};
+      if (nyq_wave) {
+        const float4 wn = ct[N / 2];
+        alpha_n = cf{wn.x, wn.y};
+        beta_n = cf{wn.z, wn.w};
+      }
+    }
+    float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);
+    float peak = 0.0f;
+    float* outb = A.out + (long long)b * A.out_stride;
+    for (int step = 0; step < nstep; ++step) {
+      const int f0 = step * FB;
+      // lane-derived offsets recomputed per step (hoisted out of the loop they are held in
+      // VGPRs through the FFTs and spill)
+      int tq = tid, ln = lane;
+      opaque_i(tq);
+      opaque_i(ln);
+      const int kb = tq & 255, kp = (N - kb) & (N - 1), m0 = 4 * ln;
+#ifdef AVZ_STAMPS
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      AVZ_STAMP(13);
+#endif
+      const uint32_t* MW = A.mwords + ((long long)b * A.nchunk + step) * F;
+      const uint32_t bits = (PF == PF_IBM_TARGET) ? MW[kb] : 0u;
+      const uint32_t bits_n = (PF == PF_IBM_TARGET && nyq_wave) ? MW[N / 2] : 0u;
+      window_fft<N, true>(v, wc, fft, slot_ptr<N>(lds, my_slot), lm);
+      window_fft<N, true>(vq, wc, fft, slot_ptr<N>(lds, my_slot + RSTRIDE), lm);
+      AVZ_STAMP(4);
+      lds_barrier();
+      AVZ_STAMP(8);
+      auto gain = [&](uint32_t bb, int i, int t) -> float {  // i: frame bit in the chunk
+        if (t >= T) return 0.0f;
+        if constexpr (PF == PF_IBM_TARGET) return ((bb >> i) & 1u) ? 0.0f : 1.0f;
+        return 1.0f;
+      };
+      // ---- apply w^H y + post-filter; frames (2p, 2p + 1) packed as Sa + i Sb into slot 2p
+      {
+        cf za[PPT], zap[PPT], zb[PPT], zbp[PPT];
+#pragma unroll
+        for (int q = 0; q < PPT; ++q) {
+          const cf* Za = slot_ptr<N>(lds, 2 * (p0 + q));
+          const cf* Zb = slot_ptr<N>(lds, 2 * (p0 + q) + 1);
+          za[q] = lds_read(Za + kb);
+          zap[q] = lds_read(Za + kp);
+          zb[q] = lds_read(Zb + kb);
+          zbp[q] = lds_read(Zb + kp);
+        }
+#pragma unroll
+        for (int q = 0; q < PPT; ++q) {
+          const int p = p0 + q, ta = f0 + 2 * p;
+          cf* Za = slot_ptr<N>(lds, 2 * p);
+          const cf sa = apply_bin(alpha, beta, za[q], zap[q], gain(bits, 2 * p, ta));
+          const cf sb = apply_bin(alpha, beta, zb[q], zbp[q], gain(bits, 2 * p + 1, ta + 1));
+          Za[kp] = {sa.x + sb.y, sb.x - sa.y};  // conj(Sa) + i conj(Sb) at N - k
+          Za[kb] = (kb == 0) ? cf{sa.x, sb.x} : cf{sa.x - sb.y, sa.y + sb.x};
+        }
+      }
+      if (nyq_wave && lane < NPAIR) {  // Nyquist bin: frame pair `lane`
+        const int ta = f0 + 2 * lane;
+        if (ta < T) {
+          cf* Za = slot_ptr<N>(lds, 2 * lane);
+          const cf* Zb = slot_ptr<N>(lds, 2 * lane + 1);
+          const float ga = gain(bits_n, 2 * lane, ta), gb = gain(bits_n, 2 * lane + 1, ta + 1);
+          const cf za = Za[N / 2], zb = Zb[N / 2];
+          Za[N / 2] = {apply_bin(alpha_n, beta_n, za, za, ga).x,
+                       apply_bin(alpha_n, beta_n, zb, zb, gb).x};
+        }
+      }
+      AVZ_STAMP(5);
+      lds_barrier();
+      AVZ_STAMP(10);
+      // ---- inverse of pair p = my_slot (every lane group): windowed contributions of
+      // frames 2p (real part) and 2p + 1 (imaginary part) into slot 2p + 1
+      {
+        const int p = my_slot;
+        cf* Zi = slot_ptr<N>(lds, 2 * p);
+        cf u[PPL];
+        static_for<0, PPL>([&](auto r) { u[r] = c_conj(Zi[lm.in0 + C::IN_STRIDE * r]); });
+        float* Cp = reinterpret_cast<float*>(slot_ptr<N>(lds, 2 * p + 1));
+        fft.forward_emit(u, Zi, [&](auto k, cf x) {
+          constexpr float ck = W32::c[k], sk = -W32::s[k];  // cos, sin of 2 pi k / 32
+          const float w = fmaf(wc.ss, sk, fmaf(-wc.sc, ck, wc.s0));
+          const int n = lm.out0 + C::OUT_STRIDE * k;
+          Cp[n] = x.x * w;
+          Cp[N + n] = -x.y * w;
+        });
+      }
+      AVZ_STAMP(7);
+      // the next step's (or utterance's) loads fly through the overlap-add (issued before
+      // the apply they held 64 more VGPRs through it and spilled 80-96 B; after the apply,
+      // through the inverse, 0.5-0.8 us slower, profiles/r04/ab_synth_utt512.txt)
+      if (step + 1 < nstep) {
+        load_step(r0, r1, f0 + FB);
+      } else {
+        load_step(n0, n1, 0);  // empty descriptors when this is the block's last utterance
+      }
+      lds_barrier();
+      AVZ_STAMP(9);
+      // ---- overlap-add: segment j = f0 - 1 + s = frame s-1 (2nd half) + frame s (1st half)
+      auto cframe = [&](int f) -> const float* {
+        return reinterpret_cast<const float*>(slot_ptr<N>(lds, 2 * (f >> 1) + 1)) + (f & 1) * N;
+      };
+      auto ola = [&]() {
+#pragma unroll
+        for (int si = 0; si < SPT; ++si) {
+          const int s = sgrp + si * NSG;
+          const int j = f0 - 1 + s;
+          if (j >= 0 && j <= T - 2) {
+            const float4 vb = *reinterpret_cast<const float4*>(cframe(s) + m0);
+            const float4 vp = *reinterpret_cast<const float4*>(cframe(s == 0 ? 0 : s - 1) + H + m0);
+            const float4 va = (s != 0) ? vp : carry;
+            float4 o;
+            o.x = (va.x + vb.x) * inv[0];
+            o.y = (va.y + vb.y) * inv[1];
+            o.z = (va.z + vb.z) * inv[2];
+            o.w = (va.w + vb.w) * inv[3];
+            *reinterpret_cast<float4*>(outb + (long long)j * H + m0) = o;
+            peak = fmaxf(peak, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+          }
+        }
+      };
+      if (rs_out != nullptr && rs_done < rs_n4) {
+        const int lo = rs_done, hi = min(rs_n4, rs_done + RS_U * kUtt512Threads);
+        rescale_slice(std::integral_constant<int, RS_U>{}, lo, hi, ola);
+        rs_done = hi;
+      } else {
+        ola();
+      }
+      if (sgrp == 0) carry = *reinterpret_cast<const float4*>(cframe(FB - 1) + H + m0);
+      lds_barrier();
+      AVZ_STAMP(11);
+    }
+    // ---- utterance peak; its rescale (own output, drained, L1-bypassing loads)
+    for (int o = 32; o > 0; o >>= 1) peak = fmaxf(peak, __shfl_xor(peak, o, 64));
+    if (lane == 0) red[wave] = peak;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float pk = red[0];
+#pragma unroll
+    for (int w = 1; w < G::NWAVE; ++w) pk = fmaxf(pk, red[w]);
+    if (tid == 0 && A.peak) A.peak[b] = pk;
+    if (A.normalize == NORM_PEAK) {
+      if (rs_out != nullptr) rescale_rest(std::integral_constant<int, 2 * RS_U>{});
+      rs_out = outb;
+      rs_scale = 1.0f / (pk + A.norm_eps);
+      rs_n4 = (T - 1) * H / 4;
+      rs_done = 0;
+    }
+    __syncthreads();  // red[] and the coefficient table of the next utterance
+    AVZ_STAMP(14);
+    b = nb;
+  }
+  if (rs_out != nullptr) rescale_rest(std::integral_constant<int, RS_BULK>{});
+  AVZ_STAMP(14);
+}
+
 // ================================ finalize ================================
 // Finalize blocks handle FCH consecutive chunks (N = 512: two, so a block rescales the same
 // 64 KB as N = 1024's one chunk instead of twice as many blocks moving 31 KB each).
@@ -1801,7 +2120,7 @@ extern "C" int avz_debug_set_synth_variant(int v) {
 // (B = 256: 70.7 + 4.2 vs 79.9 us, profiles/r04/ab_synth_utt.txt).
 template <int N, int PF, bool SPEC>
 static bool synth_per_utterance(const ChainArgs* a) {
-  return N == 1024 && !SPEC && (PF == PF_IBM_TARGET || PF == PF_NONE) &&
+  return (N == 1024 || N == 512) && !SPEC && (PF == PF_IBM_TARGET || PF == PF_NONE) &&
          a->normalize == NORM_PEAK && g_synth_variant.load(std::memory_order_relaxed) >= 1;
 }
 // ... and solves the utterance's bins itself (variant 2) when the chain's solve is the plain
@@ -1822,14 +2141,24 @@ template <int N, int PF, bool SPEC = false>
 static int launch_synth_finalize(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1,
                                  hipEvent_t e2, hipEvent_t e3, bool fused_solve = false) {
   if (synth_per_utterance<N, PF, SPEC>(a)) {
-    constexpr int lds = UttGeo::LDS_BYTES;
     constexpr int UPF = (PF == PF_IBM_TARGET || PF == PF_NONE) ? PF : PF_NONE;  // instantiated
-    auto kern = fused_solve ? avz_synthesis_utt_kernel<UPF, true> : avz_synthesis_utt_kernel<UPF, false>;
-    if (!(fused_solve ? lds_ready<avz_synthesis_utt_kernel<UPF, true>>(lds)
-                      : lds_ready<avz_synthesis_utt_kernel<UPF, false>>(lds)))
-      return -3;
     const dim3 grid((unsigned)std::min(a->batch, resident_cus()));
-    hipExtLaunchKernelGGL(kern, grid, dim3(kUttThreads), lds, st, e0, e1, 0, *a);
+    if constexpr (N == 1024) {
+      constexpr int lds = UttGeo::LDS_BYTES;
+      auto kern = fused_solve ? avz_synthesis_utt_kernel<UPF, true> : avz_synthesis_utt_kernel<UPF, false>;
+      if (!(fused_solve ? lds_ready<avz_synthesis_utt_kernel<UPF, true>>(lds)
+                        : lds_ready<avz_synthesis_utt_kernel<UPF, false>>(lds)))
+        return -3;
+      hipExtLaunchKernelGGL(kern, grid, dim3(kUttThreads), lds, st, e0, e1, 0, *a);
+    } else {
+      constexpr int lds = Utt512Geo::LDS_BYTES;
+      auto kern = fused_solve ? avz_synthesis_utt512_kernel<UPF, true>
+                              : avz_synthesis_utt512_kernel<UPF, false>;
+      if (!(fused_solve ? lds_ready<avz_synthesis_utt512_kernel<UPF, true>>(lds)
+                        : lds_ready<avz_synthesis_utt512_kernel<UPF, false>>(lds)))
+        return -3;
+      hipExtLaunchKernelGGL(kern, grid, dim3(kUtt512Threads), lds, st, e0, e1, 0, *a);
+    }
     (void)e2;  // no finalize launch: its events stay unrecorded (avz_chain_kernels)
     (void)e3;
     return 0;
@@ -1944,15 +2273,20 @@ extern "C" int avz_launch_srp(int n_fft, const ChainArgs* a, const SrpArgs* s, v
   return -4;
 }
 
+template <int N>
+static void chain_kernels_t(const ChainArgs* a, bool& utt, bool& fused) {
+  if (a->postfilter == PF_IBM_TARGET) {
+    utt = synth_per_utterance<N, PF_IBM_TARGET, false>(a);
+    fused = solve_fused<N, PF_IBM_TARGET>(a);
+  } else if (a->postfilter == PF_NONE) {
+    utt = synth_per_utterance<N, PF_NONE, false>(a);
+    fused = solve_fused<N, PF_NONE>(a);
+  }
+}
 extern "C" int avz_chain_kernels(int n_fft, const ChainArgs* a) {
   bool utt = false, fused = false;
-  if (n_fft == 1024 && a->postfilter == PF_IBM_TARGET) {
-    utt = synth_per_utterance<1024, PF_IBM_TARGET, false>(a);
-    fused = solve_fused<1024, PF_IBM_TARGET>(a);
-  } else if (n_fft == 1024 && a->postfilter == PF_NONE) {
-    utt = synth_per_utterance<1024, PF_NONE, false>(a);
-    fused = solve_fused<1024, PF_NONE>(a);
-  }
+  if (n_fft == 1024) chain_kernels_t<1024>(a, utt, fused);
+  if (n_fft == 512) chain_kernels_t<512>(a, utt, fused);
   return 1 | (fused ? 0 : 2) | 4 | (utt ? 0 : 8);
 }
 
