@@ -298,12 +298,15 @@ def test_ipd_identical_channels(avz, gpu_device):
           f"{len(dev_bins)} bins, all angle ties (|d angle| < 1e-6 rad)")
 
 
-def test_multi_round_ragged_batch_equals_single_runs(avz, gpu_device):
-    """A batch larger than one pass of the persistent grids (300 utterances of up to 4
-    chunks: 1200 items over the resident blocks, so each block loops over several items of
-    different utterances and lengths) with ragged lengths. Every utterance must equal its
-    own single-utterance run bitwise (same kernels, same per-utterance arithmetic) and the
-    peak-normalised output must peak at peak / (peak + eps)."""
+@pytest.mark.parametrize("mask,n_fft", [("ibm", 1024), ("ibm", 512), ("ipd", 1024)])
+def test_multi_round_ragged_batch_equals_single_runs(avz, gpu_device, mask, n_fft):
+    """A batch larger than one pass of the persistent grids (300 utterances against 256
+    per-utterance synthesis blocks and 2-3 analysis blocks per CU, so blocks loop over
+    several utterances / items of different lengths) with ragged lengths, for both
+    per-utterance synthesis kernels (N = 1024, 512) and the IPD plan (no post-filter). Every
+    utterance must equal its own single-utterance run bitwise (same kernels, same
+    per-utterance arithmetic) and the peak-normalised output must peak at peak / (peak +
+    eps)."""
     from avz import synth
     B, S = 300, 64000
     dm, dt, di = synth.make_batch_device(B, start=77, n_samples=S, n_interferers=2,
@@ -311,17 +314,19 @@ def test_multi_round_ragged_batch_equals_single_runs(avz, gpu_device):
     rng = np.random.default_rng(5)
     lens = rng.integers(2000, S + 1, size=B).astype(np.int32)
     lens[:3] = [S, 1024, 16001]
-    plan = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
-                        normalize="peak", max_batch=B, max_samples=S)
+    kw = dict(n_fft=n_fft, sigma=1.0 if mask == "ibm" else 1e-7, mic_d=0.01, mask=mask,
+              postfilter="ibm" if mask == "ibm" else "none", normalize="peak", max_samples=S)
+    plan = avz.MVDRPlan(max_batch=B, **kw)
     lt = torch.from_numpy(lens).to(gpu_device)
-    out, peak = plan.run(dm, lt, max_len=S, ref_tgt=dt, ref_int=di)
+    refs = dict(ref_tgt=dt, ref_int=di) if mask == "ibm" else {}
+    out, peak = plan.run(dm, lt, max_len=S, **refs)
     out, peak = out.clone(), peak.clone()
-    one = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
-                       normalize="peak", max_batch=1, max_samples=S)
+    one = avz.MVDRPlan(max_batch=1, **kw)
     for b in (0, 1, 2, 127, 128, 129, 200, 255, 256, 299):
         L = int(lens[b])
-        o1, p1 = one.run(dm[b:b + 1, :, :L].contiguous(), ref_tgt=dt[b:b + 1, :L].contiguous(),
-                         ref_int=di[b:b + 1, :L].contiguous())
+        r1 = (dict(ref_tgt=dt[b:b + 1, :L].contiguous(), ref_int=di[b:b + 1, :L].contiguous())
+              if mask == "ibm" else {})
+        o1, p1 = one.run(dm[b:b + 1, :, :L].contiguous(), **r1)
         n = one.out_len(L)
         # bitwise, NaN included: an utterance whose whole output is 0 normalises to 0/0
         # as the reference's s_out / max|s_out| does (norm_eps 0)
