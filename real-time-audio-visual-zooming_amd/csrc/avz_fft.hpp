@@ -460,7 +460,7 @@ struct Fft512x2 {
       scratch[k * 34 + j] = x;
     });
     __builtin_amdgcn_wave_barrier();
-    static_for<0, 16>([&](auto r) { v[r] = scratch[k1 * 34 + 2 * r + h2]; });
+    static_for<0, 16>([&](auto r) { v[r] = lds_read(scratch + k1 * 34 + 2 * r + h2); });  // unpaired
     __builtin_amdgcn_wave_barrier();
     dft16(v);
     xhalf_dit<16>(v, sgn, emit);
@@ -486,7 +486,10 @@ struct Fft512x2 {
       scratch[kc * 34 + jj] = x;
     });
     __builtin_amdgcn_wave_barrier();
-    static_for<0, 16>([&](auto r) { v[r] = scratch[kk * 34 + 2 * r + hh]; });
+    // unpaired reads: the compiler's ds_read2_b64 pairs bank modulo 32 in 16-lane groups,
+    // where the rows 34 complex values apart put lanes kk and kk + 8 on the same banks
+    // (2-way conflicts); single ds_read_b64 bank modulo 64 in 32-lane groups: conflict-free
+    static_for<0, 16>([&](auto r) { v[r] = lds_read(scratch + kk * 34 + 2 * r + hh); });
     __builtin_amdgcn_wave_barrier();
     dft16(v);
     xhalf_dit<16>(v, sg, emit);
@@ -498,7 +501,7 @@ struct Fft512x2 {
     static_for<1, 16>([&](auto k) { v[k] = c_mul(v[k], tw[k - 1]); });
     static_for<0, 16>([&](auto k) { scratch[k * 34 + j] = v[k]; });
     __builtin_amdgcn_wave_barrier();
-    static_for<0, 16>([&](auto r) { v[r] = scratch[k1 * 34 + 2 * r + h2]; });
+    static_for<0, 16>([&](auto r) { v[r] = lds_read(scratch + k1 * 34 + 2 * r + h2); });  // unpaired
     __builtin_amdgcn_wave_barrier();
     dft16(v);
     xhalf_dit<16>(v, sgn);
