@@ -1245,8 +1245,10 @@ __device__ __forceinline__ void synthesis_item(const ChainArgs& A, unsigned char
       }
       const int j = f0 - 1 + s;
       if (j <= T - 2) {
-        const float4 va =
-            (s == 0) ? carry : *reinterpret_cast<const float4*>(cframe(s - 1) + H + m0);
+        // unconditional read + value select: the conditional read compiled to four
+        // bank-conflicting ds_read_b32 (as in the per-utterance kernel)
+        const float4 vp = *reinterpret_cast<const float4*>(cframe(s == 0 ? 0 : s - 1) + H + m0);
+        const float4 va = (s == 0) ? carry : vp;
         float4 o;
         o.x = (va.x + vb.x) * inv[0];
         o.y = (va.y + vb.y) * inv[1];
