@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N = 1: skip the secondary configurations")
+    ap.add_argument("--secondary", default="",
+                    help="N = 1: comma-separated subset of the secondary entries to run "
+                         "(default: all)")
     ap.add_argument("--single-batch", action="store_true",
                     help="time one batch over and over instead of alternating two")
     ap.add_argument("--n-fft", type=int, choices=(512, 1024), default=1024,
@@ -139,7 +142,23 @@ def _cpu_worker(args):
     return n, bins, time.perf_counter() - t0
 
 
-def cpu_baseline(sample, seconds, workers, workload, n_fft, available):
+def cpu_share():
+    """Host cores this process may use: the cgroup CPU quota (cpu.max, cgroup v2) when one
+    is set, else the affinity mask. On the MI355X boxes the affinity mask lists the whole
+    machine while the job's share is CPU_SHARE cores per GPU."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    return affinity, quota
+
+
+def cpu_baseline(sample, seconds, workers, workload, n_fft, available, quota=None):
     """The oracle restatement of the same path (oracle/avz_oracle.py, kind 'port') on the
     host cores, time-boxed, one single-threaded worker process per core: the
     loop-faithful oracle_debug (ibm) or the vectorised masked_mvdr (ipd)."""
@@ -158,16 +177,23 @@ def cpu_baseline(sample, seconds, workers, workload, n_fft, available):
             vec = sum(r[1] for r in rv) / max(r[2] for r in rv)
     utts = sum(r[0] for r in res)
     bins = sum(r[1] for r in res)
+    value = bins / max(r[2] for r in res)
     what = ("vectorised restatement of masked_mvdr.main (IPD mask, sigma 1e-7)"
             if workload == "ipd" else
             "loop-faithful restatement of oracle_debug.main (oracle IBM, sigma 1)")
-    return {"value": bins / max(r[2] for r in res), "unit": "TF-bins/s", "cores": workers,
-            "cores_available": available, "kind": "port", "value_vectorised": vec,
+    share = min(CPU_SHARE, available)
+    return {"value": value, "unit": "TF-bins/s", "cores": workers,
+            "cores_available": share, "affinity_cores": available, "cgroup_cpu_quota": quota,
+            "kind": "port", "value_vectorised": vec, "value_per_core": value / workers,
+            "value_affinity_cores_extrapolated": value / workers * available,
             "sample": (f"time-boxed {seconds:.0f} s x {workers} single-threaded workers over "
                        f"{sample[0].shape[0]} distinct utterances of the same workload (4.0 s, "
                        f"{n_fft}/{n_fft // 2}): {utts} utterances; {what} minus WAV I/O; wall "
-                       f"{wall:.1f} s; {workers} of the {available} cores the process may run "
-                       f"on: the box's CPU share per GPU is {CPU_SHARE}"
+                       f"{wall:.1f} s; cores_available = the job's CPU share per GPU on the "
+                       f"MI355X boxes ({CPU_SHARE}; the affinity mask lists the machine's "
+                       f"{available}, and the boxes' rules size worker pools to the share); "
+                       "value_affinity_cores_extrapolated = value_per_core x affinity_cores, "
+                       "the figure all affinity cores would reach at linear scaling"
                        + ("; value_vectorised: the vectorised restatement (oracle_debug_vec), "
                           "same workers, half the time box" if vec is not None else ""))}
 
@@ -233,10 +259,23 @@ def setup_chain(spec, dev, batches):
 
     n_out = plan.out_len(S)
     F, T = n_fft // 2 + 1, -(-S // hop) + 1
+    nch = -(-T // 32)
     s0 = sets[0]
+    ibm = spec["workload"] == "ibm"
+    # per-kernel compulsory bytes (synthesis: the output stream) and the recompute design's
+    # bytes (+ the mixture re-read, the IBM words and the covariance partials it reads)
+    alg_syn = B * n_out * 4
+    design_syn = alg_syn + B * 2 * S * 4 + B * nch * F * 4 * (5 + (1 if ibm else 0))
+    syn_name = (f"avz_synthesis_utt{'' if n_fft == 1024 else '512'}_kernel"
+                f"<{'IBM' if ibm else 'NONE'}, solve fused> (per utterance; chunk-grid "
+                "avz_synthesis_kernel for batches routed to it)")
     info = dict(plan=plan, out=s0["out"][:, :min(n_out, S)], peak=s0["peak"], bins=B * F * T,
                 alg_analysis=B * streams * S * 4, alg_chain=B * (streams * S * 4 + n_out * 4),
-                kernel=f"avz_analysis_kernel<{n_fft},{'IBM' if spec['workload'] == 'ibm' else 'IPD'}>",
+                kernel=f"avz_analysis_kernel<{n_fft},{'IBM' if ibm else 'IPD'}>",
+                alg_kernel={"synthesis": alg_syn, "finalize": alg_syn},
+                design_kernel={"synthesis": design_syn, "finalize": 2 * alg_syn},
+                kernel_names={"synthesis": syn_name, "solve": f"avz_solve_kernel<{n_fft}>",
+                              "finalize": f"avz_finalize_kernel<{n_fft}>"},
                 mix=s0["mix"], refs=s0["refs"], sets=sets, it=it)
     return step, info
 
@@ -385,6 +424,143 @@ def setup_spectral(n_items, dev, n_sets):
                       kernel="avz_spectral_kernel<1024,MVDR,EXT_FLOOR> (+ batch-fallback fixup)")
 
 
+SWEEP_B = (1, 64, 200, 255, 256, 257, 300, 384)  # configs[1]'s chain at other batch sizes
+
+
+def batch_sweep(dev, args, n_sets, K, W):
+    """configs[1]'s chain (4.0 s, 2 interferers, oracle IBM, 1024/512, peak normalisation)
+    at the batch sizes of SWEEP_B, measured as the headline: value, ms per step, the kernels'
+    ms, and the rate relative to B = 256 (all utterances are 4.0 s, so TF-bins/s is
+    proportional to utterances/s). The reference's batch driver takes any --n
+    (Final_pipeline/batch_run.py:12,53, default 10)."""
+    import torch
+    res = {}
+    for B in SWEEP_B:
+        try:
+            sp = dict(workload="ibm", B=B, k=2, n_fft=1024, normalize="peak")
+            bs = [gen_batch(sp, dev, i * B, args.scenes) for i in range(n_sets)]
+            st, inf = setup_chain(sp, dev, bs)
+            el, ktx, _ = run_timed(st, inf["plan"], K, W, 1, dev, not args.no_settle,
+                                   not args.no_kernel_timing)
+            e = {"value": inf["bins"] * K / el, "ms_per_step": 1e3 * el / K,
+                 "tf_bins_per_step": inf["bins"]}
+            if ktx:
+                e["kernels_ms"] = {k: ktx[k] for k in inf["plan"].KERNELS}
+            res[str(B)] = e
+            del bs, st, inf
+            torch.cuda.empty_cache()
+        except Exception as exc:  # a side figure must never sink the bench line
+            res[str(B)] = {"error": repr(exc)[:300]}
+    ref = res.get("256", {}).get("value")
+    if ref:
+        for e in res.values():
+            if "value" in e:
+                e["rate_vs_b256"] = e["value"] / ref
+        ge = [e["rate_vs_b256"] for b, e in res.items() if int(b) >= 256 and "value" in e]
+        res["min_rate_vs_b256_for_b_ge_256"] = min(ge) if ge else None
+    res["config"] = ("configs[1] chain at batch B in " + str(list(SWEEP_B)) + ": 4.0 s, 2 "
+                     "interferers, oracle IBM, 1024/512, peak normalisation; rate_vs_b256 = "
+                     "value / value at B = 256")
+    return res
+
+
+def configs0_latency(dev, n_calls=50):
+    """configs[0]: ONE mixture through oracle_debug (rt_av_zoom/core/oracle_debug.py:27-97),
+    the bundled 8.23-s test triple (tests/golden/inputs_test.npz, int16 / 32768 as the
+    reference reads it), at 512/256 (as shipped) and 1024/512, sigma 1: the engine's time per
+    call (back to back, and call + synchronize as a real-time caller sees it) beside the
+    loop-faithful CPU oracle on the same triple (one core), and the output's SIR against the
+    reference-run golden (full_test_n{N}_s1.npz)."""
+    import torch
+    from threadpoolctl import threadpool_limits
+
+    import avz
+    from oracle import avz_oracle as O
+    gdir = os.path.join(ROOT, "tests", "golden")
+    with np.load(os.path.join(gdir, "inputs_test.npz"), allow_pickle=False) as z:
+        f = lambda a: (a.astype(np.float64) / 32768.0).astype(np.float32)  # noqa: E731
+        mix, tgt, itf = f(z["mix"]).T.copy(), f(z["tgt"]), f(z["int"])
+    S = len(tgt)
+    res = {"config": ("configs[0]: one mixture (bundled test triple, 8.23 s, 1 interferer), "
+                      "oracle IBM, sigma 1, B = 1"), "samples": S}
+    for n in (512, 1024):
+        plan = avz.MVDRPlan(n_fft=n, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
+                            normalize="peak", max_batch=1, max_samples=S)
+        d_mix = torch.from_numpy(mix).to(dev)[None]
+        d_t, d_i = torch.from_numpy(tgt).to(dev)[None], torch.from_numpy(itf).to(dev)[None]
+        lens = torch.full((1,), S, dtype=torch.int32, device=dev)
+        out = plan.alloc_out(1, S, dev)
+        peak = torch.empty((1,), dtype=torch.float32, device=dev)
+
+        def call():
+            plan.run(d_mix, lens, max_len=S, out=out, peak=peak, ref_tgt=d_t, ref_int=d_i)
+        for _ in range(20):
+            call()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n_calls):
+            call()
+        torch.cuda.synchronize()
+        pipelined = 1e3 * (time.perf_counter() - t0) / n_calls
+        lat = []
+        for _ in range(n_calls):
+            t0 = time.perf_counter()
+            call()
+            torch.cuda.synchronize()
+            lat.append(1e3 * (time.perf_counter() - t0))
+        plan.set_timing(True)
+        for _ in range(10):
+            call()
+        kt = plan.timing()
+        plan.set_timing(False)
+        # the round-3 synthesis form for comparison: chunk grid + solve + finalize launches
+        # (avz_debug_set_synth_variant(0); the analysis kernel as above)
+        from avz._lib import lib as _lib
+        alt = None
+        if hasattr(_lib, "avz_debug_set_synth_variant") and _lib.avz_debug_set_synth_variant(0) == 0:
+            try:
+                for _ in range(10):
+                    call()
+                torch.cuda.synchronize()
+                lat0 = []
+                for _ in range(n_calls):
+                    t0 = time.perf_counter()
+                    call()
+                    torch.cuda.synchronize()
+                    lat0.append(1e3 * (time.perf_counter() - t0))
+                alt = float(np.median(lat0))
+            finally:
+                _lib.avz_debug_set_synth_variant(2)
+        call()
+        torch.cuda.synchronize()
+        n_out = plan.out_len(S)
+        got = out[0, :n_out].cpu().numpy().astype(np.float64)
+        with np.load(os.path.join(gdir, f"full_test_n{n}_s1.npz"), allow_pickle=False) as g:
+            sir_ref = float(g["sir_out"])
+        L = min(len(got), S)
+        sir = O.projection_sdr_sir(got[:L], tgt[:L], itf[:L])[1]
+        with threadpool_limits(1):
+            cpu = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                O.oracle_debug_loop(mix, tgt, itf, n_fft=n, hop=n // 2, sigma=1.0)
+                cpu.append(1e3 * (time.perf_counter() - t0))
+        F, T = n // 2 + 1, O.n_frames(S, n, n // 2)
+        res[f"n{n}"] = {
+            "ms_per_call_back_to_back": pipelined,
+            "ms_per_call_synchronous_median": float(np.median(lat)),
+            "ms_per_call_synchronous_p90": float(np.percentile(lat, 90)),
+            "kernels_ms": {k: kt[k] for k in plan.KERNELS},
+            "tf_bins": F * T, "tf_bins_per_s_back_to_back": F * T / (pipelined * 1e-3),
+            "sir_out_db": float(sir), "sir_out_reference_db": sir_ref,
+            "sir_abs_delta_db": abs(float(sir) - sir_ref),
+            "ms_per_call_synchronous_chunk_grid_synthesis": alt,
+            "cpu_oracle_loop_ms_median_1core": float(np.median(cpu)),
+            "speedup_vs_cpu_1core_synchronous": float(np.median(cpu) / np.median(lat))}
+        del plan
+    return res
+
+
 def run_timed(step, plan, K, W, world, dev, settle_on, kernel_timing):
     """Clock settling, W warmup steps, K timed steps (barrier + synchronize on both sides),
     then an untimed pass with HIP events around all four kernels."""
@@ -485,12 +661,16 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.workload != "unet":
-        available = len(os.sched_getaffinity(0))
-        workers = args.cpu_workers or min(CPU_SHARE, available)
+        available, quota = cpu_share()
+        share = min(CPU_SHARE, available)
+        if quota is not None:
+            share = max(1, min(share, int(quota)))
+        workers = args.cpu_workers or share
         k = min(B, 32)
         # the host restatement of the same scenes (forked before any GPU initialisation)
         sample = gen_host(k, start=rank * B, n_samples=S, n_interferers=args.interferers)
-        cpu = cpu_baseline(sample, args.cpu_seconds, workers, args.workload, N_FFT, available)
+        cpu = cpu_baseline(sample, args.cpu_seconds, workers, args.workload, N_FFT, available,
+                           quota)
 
     import torch
     import torch.distributed as dist
@@ -641,16 +821,36 @@ def main():
         dom_ms = kt["analysis_timed"]  # HIP events on the launch stream, over the timed steps
         roof["kernels_ms"] = {k: kt[k] for k in plan.KERNELS}  # separate untimed pass
         roof["kernels_ms_note"] = ("kernels_ms: the four kernels in an untimed pass after the "
-                                   "timed steps; dominant_kernel.kernel_ms: the analysis kernel "
+                                   "timed steps; analysis_kernel.kernel_ms: the analysis kernel "
                                    f"on every {TIMING_PERIOD}th timed step "
                                    f"({kt['analysis_timed_calls']} of {K} launches), HIP events "
                                    "carried by its dispatch on the launch stream")
-        roof["dominant_kernel"] = {
-            "kernel": info["kernel"], "kernel_ms": dom_ms,
-            "alg_bytes_per_launch": alg_analysis,
-            "achieved": alg_analysis / (dom_ms * 1e-3) / 1e9,
-            "frac": alg_analysis / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "traffic": traffic.get("analysis")}
+        ana = {"kernel": info["kernel"], "kernel_ms": dom_ms,
+               "alg_bytes_per_launch": alg_analysis,
+               "achieved": alg_analysis / (dom_ms * 1e-3) / 1e9,
+               "frac": alg_analysis / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+               "traffic": traffic.get("analysis")}
+        roof["analysis_kernel"] = ana
+        # the kernel that bounds the step: the longest of the untimed pass
+        name = max(plan.KERNELS, key=lambda k: kt[k] if kt[k] == kt[k] else -1.0)
+        if name == "analysis":
+            roof["dominant_kernel"] = dict(ana, role="analysis")
+        else:
+            ms = kt[name]
+            alg = info["alg_kernel"].get(name, 0)
+            design = info["design_kernel"].get(name, alg)
+            roof["dominant_kernel"] = {
+                "kernel": info["kernel_names"].get(name, name), "role": name, "kernel_ms": ms,
+                "alg_bytes_per_launch": alg,
+                "achieved": alg / (ms * 1e-3) / 1e9,
+                "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "design_bytes_per_launch": design,
+                "frac_design": design / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "traffic": traffic.get(name),
+                "note": ("alg: its compulsory bytes (the output stream); design: + the mixture "
+                         "re-read of the recompute design (the forward FFT is recomputed "
+                         "instead of storing Y), the IBM words and the covariance partials; "
+                         "kernel_ms from the untimed all-kernel pass")}
         roof["chain_events"] = {"ms": chain_ms, "alg_bytes_per_launch": alg_chain,
                                 "achieved": alg_chain / (chain_ms * 1e-3) / 1e9,
                                 "frac": alg_chain / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
@@ -681,7 +881,20 @@ def main():
                                      text=WORKLOAD_TEXT["unet"].format(B=1024, unet_dtype="fp32",
                                                                        n=1024, h=512))),
         ]
+        only = set(x for x in args.secondary.split(",") if x)
+        want = lambda name: not only or name in only  # noqa: E731
+        if want("configs[0]_latency"):
+            try:
+                secondary["configs[0]_latency"] = configs0_latency(dev)
+            except Exception as exc:  # a side figure must never sink the bench line
+                secondary["configs[0]_latency"] = {"error": repr(exc)[:300]}
+            torch.cuda.empty_cache()
+        if want("batch_sweep"):
+            secondary["batch_sweep"] = batch_sweep(dev, args, n_sets, K, args.warmup)
+        specs = [x for x in specs if want(x[0])]
         try:  # the spectral-domain operator on a 4096-item chunk batch (configs[4]'s items)
+            if not want("spectral_4096"):
+                raise StopIteration
             st, inf = setup_spectral(4096, dev, n_sets)
             el, _, _ = run_timed(st, inf["plan"], K, args.warmup, 1, dev, not args.no_settle,
                                  False)
@@ -700,6 +913,8 @@ def main():
                              "note": "step wall time / K (both launches of the call)"}}
             del st, inf
             torch.cuda.empty_cache()
+        except StopIteration:
+            pass
         except Exception as exc:  # a side figure must never sink the bench line
             secondary["spectral_4096"] = {"error": repr(exc)[:300]}
         for name, sp in specs:

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as ct
 import os
+import warnings
 
 # PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7). Loading torch
 # first makes libavz.so's NEEDED libamdhip64.so.7 resolve to that same runtime, so
@@ -165,8 +166,16 @@ def _load():
     # diagnostic A/B of the synthesis paths (tools/ab_synth.py, bench.py runs): 2 the
     # per-utterance kernel solving its own bins (default), 1 the same after the solve
     # kernel, 0 the chunk grid + finalize
-    if os.environ.get("AVZ_SYNTH_VARIANT") and hasattr(lib, "avz_debug_set_synth_variant"):
-        lib.avz_debug_set_synth_variant(int(os.environ["AVZ_SYNTH_VARIANT"]))
+    v = os.environ.get("AVZ_SYNTH_VARIANT")  # diagnostic A/B only (tools/gpu_bench_ab.sh)
+    if v and hasattr(lib, "avz_debug_set_synth_variant"):
+        try:
+            ok = lib.avz_debug_set_synth_variant(int(v)) == 0
+        except ValueError:
+            ok = False
+        if not ok:
+            warnings.warn(f"AVZ_SYNTH_VARIANT={v!r} ignored (expected 0, 1 or 2)")
+        else:
+            warnings.warn(f"AVZ_SYNTH_VARIANT={v}: synthesis path overridden for this process")
     return lib
 
 

@@ -123,19 +123,18 @@ class NeuralMaskBeamformer:
     runs in bf16, the mask is handed to the HIP chain in fp32). ``channels_last``: NHWC
     activations for the convolutions (fp32 results equal to within 1e-7 of NCHW on MI355X,
     ~3 % faster forward; tools/unet_speed.py). ``fold_bn``: an eval-mode model runs as its
-    BatchNorm-folded copy (fold_batchnorm)."""
+    BatchNorm-folded copy (fold_batchnorm): the beamformer then holds a SNAPSHOT of the
+    weights, so later load_state_dict calls or edits on the caller's model are not seen --
+    call ``refresh(model)`` after changing it (or pass fold_bn=False to run the caller's
+    module itself)."""
 
     def __init__(self, model: nn.Module, max_items: int, conf: dict | None = None,
                  model_batch: int = 256, model_dtype=torch.float32, channels_last: bool = True,
                  fold_bn: bool = True):
         conf = conf or CONF
-        if fold_bn and not model.training and any(
-                isinstance(x, nn.BatchNorm2d) for x in model.modules()):
-            model = fold_batchnorm(model)
+        self.fold_bn = fold_bn
         self.channels_last = channels_last
-        if channels_last:
-            model = model.to(memory_format=torch.channels_last)
-        self.model = model
+        self.refresh(model)
         self.chunk = int(conf["train_seg_samples"])
         self.hop_c = self.chunk // 2
         self.model_batch = model_batch
@@ -147,6 +146,16 @@ class NeuralMaskBeamformer:
                              max_batch=max_items, max_samples=self.chunk)
         # main_deploy keeps the first min(len(out_chunk), WIN_SIZE) samples (:151-153)
         self.item_out_len = min(self.plan.out_len(self.chunk), self.chunk)
+
+    def refresh(self, model: nn.Module) -> None:
+        """(Re)build the module the forward runs from ``model``: its BatchNorm-folded copy
+        (fold_bn, eval mode), in channels-last memory format if requested."""
+        if self.fold_bn and not model.training and any(
+                isinstance(x, nn.BatchNorm2d) for x in model.modules()):
+            model = fold_batchnorm(model)
+        if self.channels_last:
+            model = model.to(memory_format=torch.channels_last)
+        self.model = model
 
     @torch.no_grad()
     def masks(self, items: torch.Tensor) -> torch.Tensor:

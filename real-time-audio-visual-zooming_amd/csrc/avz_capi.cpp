@@ -1,6 +1,7 @@
 // avz_capi.cpp — plan management, validation and dispatch behind include/avz.h.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <complex>
 #include <limits>
@@ -24,7 +25,21 @@ struct Workspace {
   uint32_t* peak_u;
   int* flag;                 // [batch] item-level fallback flags (AVZ_FALLBACK_BATCH)
   float* pf_gain;            // [batch][nchunk][32][F] IRM gains (AVZ_PF_IRM plans only)
+  float* tpart;              // [tail_slots][5][F] analysis pieces' partials (tail splitting)
+  int tail_slots;
+  float* pheads;             // [seam_slots][H] per-utterance synthesis pieces' seam halves
+  float* ptails;
+  int seam_slots;
 };
+
+// Tail-splitting capacity (ChainArgs a_* / s_*): analysis pieces of a partial last round
+// (at most the analysis grid, 3 blocks x 256 CUs; 8 pieces per 32-frame chunk), and the
+// seams of the per-utterance synthesis pieces (at most 255 piece utterances on 256 CUs,
+// 32 pieces each, at most two per chunk). Launches never split beyond these.
+static int tail_slots(long long B, int nchunk) { return (int)std::min<long long>(B * nchunk * 8, 768); }
+static int seam_slots(long long B, int nchunk) {
+  return (int)(std::min<long long>(B, 256) * std::min(32, 2 * nchunk));
+}
 
 static size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
 
@@ -40,6 +55,9 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
   const size_t sz_b = align256(sizeof(uint32_t) * B);
   const size_t sz_gain =
       c.postfilter == AVZ_PF_IRM ? align256(sizeof(float) * B * nchunk * CF * F) : 0;
+  const int ts = tail_slots(B, nchunk), ss = seam_slots(B, nchunk);
+  const size_t sz_tpart = align256(sizeof(float) * (size_t)ts * 5 * F);
+  const size_t sz_seam = align256(sizeof(float) * (size_t)ss * H);
   if (base && w) {
     char* q = base;
     w->part = reinterpret_cast<float*>(q); q += sz_part;
@@ -50,8 +68,14 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
     w->peak_u = reinterpret_cast<uint32_t*>(q); q += sz_b;
     w->flag = reinterpret_cast<int*>(q); q += sz_b;
     w->pf_gain = sz_gain ? reinterpret_cast<float*>(q) : nullptr;
+    q += sz_gain;
+    w->tpart = reinterpret_cast<float*>(q); q += sz_tpart;
+    w->tail_slots = ts;
+    w->pheads = reinterpret_cast<float*>(q); q += sz_seam;
+    w->ptails = reinterpret_cast<float*>(q); q += sz_seam;
+    w->seam_slots = ss;
   }
-  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 2 * sz_b + sz_gain;
+  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 2 * sz_b + sz_gain + sz_tpart + 2 * sz_seam;
 }
 
 struct avz_plan {
@@ -325,6 +349,11 @@ static int prepare_chain(const avz_plan* p, const avz_batch_args* a, int use, av
   k.peak_u = ws.peak_u;
   k.flag = ws.flag;
   k.pf_gain = ws.pf_gain;
+  k.tpart = ws.tpart;
+  k.tpart_slots = ws.tail_slots;
+  k.pheads = ws.pheads;
+  k.ptails = ws.ptails;
+  k.pseam_slots = ws.seam_slots;
   if (use == USE_COVARIANCE) {  // that stage produces cov_out only: leave the caller's
     k.out = nullptr;            // out / peak / w buffers untouched (the analysis kernel
     k.peak = nullptr;           // would otherwise zero peak[b] as the atomicMax target)

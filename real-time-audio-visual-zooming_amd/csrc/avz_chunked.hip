@@ -330,9 +330,13 @@ __device__ __forceinline__ float irm_gain(cf zr, cf zrp) {
 
 // ================================ analysis ================================
 struct NoTw {};
+// piece p of P (P = 1: the whole item) runs the chunk's steps [p SA / P, (p + 1) SA / P), SA =
+// steps per chunk; slot >= 0: its partials go to tail slot `slot` of tpart and its IBM bits
+// into the chunk's mask words atomically (the other pieces own the word's other bits).
 template <int N, int MASK, bool IRM, class TW>
 __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char* lds, int c,
-                                              int b, const TW& tw_reg, const LaneConst<N>& K) {
+                                              int b, int p, int P, int slot, const TW& tw_reg,
+                                              const LaneConst<N>& K) {
   using C = KCfg<N>;
   using G = CGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
@@ -354,13 +358,15 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
   if (c >= nch) return;
-  if (c == 0 && tid == 0) {
+  if (c == 0 && p == 0 && tid == 0) {
     A.peak_u[b] = 0u;
     if (A.peak && A.normalize != NORM_PEAK) A.peak[b] = 0.0f;  // finalize's atomicMax target
   }
   const int t0 = c * kChunk;
   const int nframes = min(kChunk, T - t0);
-  const int nstep = (nframes + FB - 1) / FB;
+  constexpr int SA = kChunk / FB;  // steps of a full chunk
+  const int s_lo = p * SA / P;      // this piece's steps [s_lo, nstep)
+  const int nstep = min((nframes + FB - 1) / FB, (p + 1) * SA / P);
 
   const typename C::Fft fft = K.fft;
   const LaneMap<N> lm = K.lm;
@@ -458,10 +464,10 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   for (int j = 0; j < BPT; ++j) wone[j] = (MASK == MASK_IPD && j == 0 && tid == 0) ? 0.0f : 1.0f;
 
   AVZ_STAMP_DECL();
-  issue_loads(0);
+  issue_loads(s_lo);
   lds_barrier();  // twiddle table
   AVZ_STAMP_INIT();
-  for (int step = 0; step < nstep; ++step) {
+  for (int step = s_lo; step < nstep; ++step) {
     const int f0 = t0 + step * FB;
     const bool live = f0 + wave_frame0 < T;  // wave-uniform: any of its frames exist
 #ifdef AVZ_STAMPS
@@ -677,9 +683,20 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     AVZ_STAMP(2);
   }
 
-  // ---- chunk partials
-  float* P = A.part + ((long long)b * A.nchunk + c) * 5 * F;
+  // ---- chunk partials (a piece's: its tail slot; its bits merged into the chunk's words)
+  float* Pt = slot < 0 ? A.part + ((long long)b * A.nchunk + c) * 5 * F
+                       : A.tpart + (long long)slot * 5 * F;
   uint32_t* MW = A.mwords + ((long long)b * A.nchunk + c) * F;
+  // the piece's bit range (nominal: bits past the chunk's frames are cleared too)
+  const uint32_t rng = (P == 1) ? ~0u : ((1u << (kChunk / P)) - 1u) << (kChunk / P * p);
+  auto put_word = [&](int k, uint32_t w) {
+    if (slot < 0) {
+      MW[k] = w;
+    } else {
+      atomicAnd(MW + k, ~rng);
+      atomicOr(MW + k, w);
+    }
+  };
   constexpr bool DC_NYQ = MASK == MASK_IPD;  // DC sums come from the Nyquist wave
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
@@ -688,12 +705,12 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     // binary weights were folded into the selects: their count is exact in fp32
     if constexpr (MASK == MASK_IBM) acc[j].cm = (float)__popc(bits[j]);
     if constexpr (MASK == MASK_IPD) acc[j].cm += (float)ipd_clear_n[j];
-    P[0 * F + kb] = acc[j].c00;
-    P[1 * F + kb] = acc[j].c11;
-    P[2 * F + kb] = acc[j].c01r;
-    P[3 * F + kb] = acc[j].c01i;
-    P[4 * F + kb] = acc[j].cm;
-    if constexpr (MASK == MASK_IBM) MW[kb] = bits[j];
+    Pt[0 * F + kb] = acc[j].c00;
+    Pt[1 * F + kb] = acc[j].c11;
+    Pt[2 * F + kb] = acc[j].c01r;
+    Pt[3 * F + kb] = acc[j].c01i;
+    Pt[4 * F + kb] = acc[j].cm;
+    if constexpr (MASK == MASK_IBM) put_word(kb, bits[j]);
   }
   if (nyq_wave) {
     for (int o = 1; o < 64; o <<= 1) {
@@ -711,26 +728,47 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
       }
     }
     if (DC_NYQ && lane == 0) {
-      P[0 * F] = adc.c00;
-      P[1 * F] = adc.c11;
-      P[2 * F] = adc.c01r;
-      P[3 * F] = adc.c01i;
-      P[4 * F] = adc.cm;
+      Pt[0 * F] = adc.c00;
+      Pt[1 * F] = adc.c11;
+      Pt[2 * F] = adc.c01r;
+      Pt[3 * F] = adc.c01i;
+      Pt[4 * F] = adc.cm;
     }
     if (lane == 0) {
-      P[0 * F + N / 2] = an.c00;
-      P[1 * F + N / 2] = an.c11;
-      P[2 * F + N / 2] = an.c01r;
-      P[3 * F + N / 2] = an.c01i;
-      P[4 * F + N / 2] = an.cm;
-      if constexpr (MASK == MASK_IBM) MW[N / 2] = nyq_bits;
+      Pt[0 * F + N / 2] = an.c00;
+      Pt[1 * F + N / 2] = an.c11;
+      Pt[2 * F + N / 2] = an.c01r;
+      Pt[3 * F + N / 2] = an.c01i;
+      Pt[4 * F + N / 2] = an.cm;
+      if constexpr (MASK == MASK_IBM) put_word(N / 2, nyq_bits);
+    }
+  }
+}
+
+// The block's work units: whole items i, i + gridDim.x, ... below a_whole (a multiple of the
+// grid), then the tail items' pieces on the same stride (tail splitting, ChainArgs).
+template <int N, int MASK, bool IRM, class TW>
+__device__ __forceinline__ void analysis_items(const ChainArgs& A, unsigned char* lds, int gx,
+                                               int n_items, const TW& tw_reg,
+                                               const LaneConst<N>& K) {
+  const int P = A.a_pieces > 1 ? A.a_pieces : 1;
+  const int n_whole = P > 1 ? A.a_whole : n_items;
+  int u = blockIdx.x;
+  for (; u < n_whole; u += gridDim.x)
+    analysis_item<N, MASK, IRM>(A, lds, u % gx, u / gx, 0, 1, -1, tw_reg, K);
+  if (P > 1) {
+    const int n_units = (n_items - n_whole) * P;
+    for (int q = u - n_whole; q < n_units; q += gridDim.x) {
+      const int it = n_whole + q / P;
+      analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, q % P, P, q, tw_reg, K);
     }
   }
 }
 
 // Persistent grid (about two blocks per CU): block i takes the (chunk, utterance) items
 // i, i + gridDim.x, ... so the twiddle table is built once per block and the batch is
-// spread evenly over the resident blocks (no second, partly idle round of short blocks).
+// spread evenly over the resident blocks (no second, partly idle round of short blocks);
+// a partial last round is split into step-range pieces (analysis_items).
 template <int N, int MASK, bool IRM>
 __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysis_kernel(ChainArgs A) {
   using G = CGeo<N>;
@@ -749,13 +787,11 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysi
     }
     LaneConst<N> K;
     K.init(threadIdx.x);
-    for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-      analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, tw_reg, K);
+    analysis_items<N, MASK, IRM>(A, lds, gx, n_items, tw_reg, K);
   } else {
     LaneConst<N> K;
     K.init(threadIdx.x);
-    for (int it = blockIdx.x; it < n_items; it += gridDim.x)
-      analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, NoTw{}, K);
+    analysis_items<N, MASK, IRM>(A, lds, gx, n_items, NoTw{}, K);
   }
 }
 
@@ -767,16 +803,40 @@ constexpr int kSolveThreads = 256;
 
 // Covariance sums of bin k of utterance b: fp64 sum of its nch chunk partials, scaled back
 // by 1/4 (the analysis accumulates (2 y)(2 y)^H).
-template <int N>
+// V: split-chunk partial vectors per round trip (the per-utterance kernels' fallback takes
+// few: its prefetched samples are live there).
+template <int N, int V = 8>
 __device__ __forceinline__ void bin_cov_sums(const ChainArgs& A, int b, int k, int nch,
                                              double (&R)[5]) {
   constexpr int F = N / 2 + 1;
   const float* P = A.part + (long long)b * A.nchunk * 5 * F + k;
 #pragma unroll
   for (int q = 0; q < 5; ++q) R[q] = 0.0;
-  for (int cc = 0; cc < nch; ++cc) {
+  // chunks of a split tail item (analysis_items) sum their pieces' partials
+  const long long it0 = (long long)b * ((A.max_frames + kChunk - 1) / kChunk);
+  const int cw = A.a_pieces > 1 ? (int)max(0LL, min((long long)nch, A.a_whole - it0)) : nch;
+  for (int cc = 0; cc < cw; ++cc) {
 #pragma unroll
     for (int q = 0; q < 5; ++q) R[q] += (double)P[((long long)cc * 5 + q) * F];
+  }
+  if (cw < nch) {
+    // the split chunks' pieces: (nch - cw) a_pieces consecutive partial vectors of tpart,
+    // V per round trip through a descriptor covering exactly them (absent ones read +0,
+    // which leaves the sums unchanged); summed in chunk and piece order
+    const int nv = (nch - cw) * A.a_pieces;
+    const rsrc_t rt =
+        make_rsrc(A.tpart + (it0 + cw - A.a_whole) * A.a_pieces * 5 * F, (long long)nv * 5 * F);
+    for (int v0 = 0; v0 < nv; v0 += V) {
+      float p[V][5];
+#pragma unroll
+      for (int i = 0; i < V; ++i)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) p[i][q] = bload_nn(rt, ((v0 + i) * 5 + q) * F + k);
+#pragma unroll
+      for (int i = 0; i < V; ++i)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) R[q] += (double)p[i][q];
+    }
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) R[q] *= 0.25;
@@ -789,6 +849,11 @@ template <int N>
 __device__ __forceinline__ void bin_cov_sums_utt(const ChainArgs& A, int b, int k, int nch,
                                                  double (&R)[5]) {
   constexpr int F = N / 2 + 1;
+  if (A.a_pieces > 1 &&
+      (long long)b * ((A.max_frames + kChunk - 1) / kChunk) + nch > A.a_whole) {
+    bin_cov_sums<N, 4>(A, b, k, nch, R);  // some of its chunks were split (block-uniform)
+    return;
+  }
   const rsrc_t rp = make_rsrc(A.part + (long long)b * A.nchunk * 5 * F, (long long)nch * 5 * F);
 #pragma unroll
   for (int q = 0; q < 5; ++q) R[q] = 0.0;
@@ -811,8 +876,8 @@ template <int N>
 __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   constexpr int H = N / 2, F = N / 2 + 1;
   const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
-  if (idx >= (long long)A.batch * F) return;
-  const int b = (int)(idx / F), k = (int)(idx % F);
+  if (idx >= (long long)(A.batch - A.b_lo) * F) return;
+  const int b = A.b_lo + (int)(idx / F), k = (int)(idx % F);  // b_lo: a piece utterances' solve
   const int L = utt_len(A, b);
   if (L < N) return;
   const int T = (L + H - 1) / H + 1;
@@ -1319,8 +1384,10 @@ __device__ __forceinline__ cf* utt_frame(unsigned char* lds, int f) {
 // SOLVE: the block solves its utterance's 513 bins itself (the MVDR solve of
 // avz_solve_kernel, one bin per thread, straight into the LDS coefficient table) instead of
 // reading the solve kernel's coef[] -- no solve launch (plain MVDR plans without the
-// item-level fallback or debug outputs).
-template <int PF, bool SOLVE>
+// item-level fallback or debug outputs). PIECES: the instance for a split batch (whole
+// utterances, then step pieces; synth_split) -- the whole-rounds instance compiles the
+// piece logic out (with it the step loop ran 92.7 -> 98.5 us at B = 256).
+template <int PF, bool SOLVE, bool PIECES>
 __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(ChainArgs A) {
   constexpr int N = UttGeo::N, H = UttGeo::H, F = UttGeo::F, FB = UttGeo::FB;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -1364,27 +1431,49 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
   AVZ_STAMP_DECL();
   AVZ_STAMP_INIT();
 
-  // the block's utterances b = blockIdx.x, + gridDim.x, ...; one with a bad device length
-  // (host validates) reports NaN, as finalize does, and is skipped
-  auto next_valid = [&](int bb) {
-    for (; bb < A.batch; bb += gridDim.x) {
-      if (utt_len(A, bb) >= N) break;
-      if (tid == 0 && A.peak) A.peak[bb] = __builtin_nanf("");
+  // The block's work units g = blockIdx.x, + gridDim.x, ...: the whole utterances g <
+  // s_whole, then the pieces q = g - s_whole of the utterances [s_whole, batch) (ChainArgs
+  // s_pieces, s_steps): utterance s_whole + q / s_pieces, its steps [p s_steps, (p + 1) s_steps),
+  // p = q % s_pieces (the host splits only a partial last round or a batch below the CU
+  // count). A whole utterance with a bad device length (host validates) reports NaN, as
+  // finalize does; such an utterance's pieces, and pieces past an utterance's last step, are
+  // skipped (the piece finalize reports the NaN).
+  const int pieces = PIECES && A.s_pieces > 0 ? A.s_pieces : 0;
+  const int s_whole = pieces > 0 ? A.s_whole : A.batch;
+  const int n_units = s_whole + (A.batch - s_whole) * pieces;
+  struct Unit {
+    int g, b, s_lo, s_hi, slot;  // slot: the piece's seam slot, -1 for a whole utterance
+  };
+  auto unit_at = [&](int g) -> Unit {
+    for (; g < n_units; g += gridDim.x) {
+      // lengths read back as block-uniform values: a loop exit decided on a vector load
+      // made the next unit's buffer descriptors divergent (a waterfall loop per load)
+      if (g < s_whole) {
+        const int Lg = __builtin_amdgcn_readfirstlane(utt_len(A, g));
+        if (Lg >= N) return Unit{g, g, 0, ((Lg + H - 1) / H + 1 + FB - 1) / FB, -1};
+        if (tid == 0 && A.peak) A.peak[g] = __builtin_nanf("");
+        continue;
+      }
+      const int q = g - s_whole, bq = s_whole + q / pieces, lo = (q % pieces) * A.s_steps;
+      const int Lq = __builtin_amdgcn_readfirstlane(utt_len(A, bq));
+      const int ns = ((Lq + H - 1) / H + 1 + FB - 1) / FB;
+      if (Lq >= N && lo < ns) return Unit{g, bq, lo, min(ns, lo + A.s_steps), q};
     }
-    return bb;
+    return Unit{n_units, A.batch, 0, 0, -1};
   };
   auto rsrcs = [&](int bb, rsrc_t& a0, rsrc_t& a1) {
+    bb = __builtin_amdgcn_readfirstlane(bb);
     const float* mixb = A.mix + (long long)bb * A.mix_stride;
-    const int len = utt_len(A, bb);
+    const int len = __builtin_amdgcn_readfirstlane(utt_len(A, bb));
     a0 = make_rsrc(mixb, len);
     a1 = make_rsrc(mixb + A.ch_stride, len);
   };
   cf v[32];
-  // step 0 of an utterance: wave 0's first frame starts N/2 before sample 0 (range-checked
-  // offsets); the other waves' frames start at sample >= 0
-  auto first_loads = [&](rsrc_t a0, rsrc_t a1) {
-    const int s0 = my * H - N / 2 + lm.in0;
-    if (wave >= 1) {
+  // a unit's first step (frames f0 ..): at f0 = 0 wave 0's first frame starts N/2 before
+  // sample 0 (range-checked offsets); every other frame starts at sample >= 0
+  auto first_loads = [&](rsrc_t a0, rsrc_t a1, int f0) {
+    const int s0 = (f0 + my) * H - N / 2 + lm.in0;
+    if (wave >= 1 || f0 > 0) {
       static_for<0, 32>([&](auto r) {
         v[r].x = bload_nn(a0, s0 + 32 * r);
         v[r].y = bload_nn(a1, s0 + 32 * r);
@@ -1396,11 +1485,11 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       });
     }
   };
-  int b = next_valid(blockIdx.x);
-  if (b < A.batch) {
+  Unit cu = unit_at(blockIdx.x);
+  if (cu.b < A.batch) {
     rsrc_t a0, a1;
-    rsrcs(b, a0, a1);
-    first_loads(a0, a1);
+    rsrcs(cu.b, a0, a1);
+    first_loads(a0, a1, PIECES ? cu.s_lo * FB : 0);
   }
   // NORM_PEAK: an utterance's rescale (its own output, L1-bypassing loads) runs spread over
   // the NEXT utterance's steps, one slice per overlap-add phase, so its memory traffic hides
@@ -1409,6 +1498,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
   float rs_scale = 0.0f;
   int rs_n4 = 0, rs_done = 0;
   constexpr int RS_U = 4;   // float4 groups per thread per slice (8 slices cover 4 s)
+  constexpr int RS_UP = 8;   // the same during a piece's steps (4 slices cover 4 s)
   constexpr int RS_BULK = 32;  // after the loop: a 4-s utterance in one round trip of loads
   auto rescale_slice = [&](auto uc, int lo, int hi, auto issue_more) {
     constexpr int U = decltype(uc)::value;
@@ -1439,22 +1529,33 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       rescale_slice(uc, rs_done, min(rs_n4, rs_done + U * kUttThreads), [] {});
     rs_out = nullptr;
   };
-  while (b < A.batch) {
-    const int L = utt_len(A, b);
+  // Across a unit's steps only b and its last step are held (more spilled): a piece is
+  // recognised by b >= s_whole, its seam slot and unit index follow from b and the frame.
+  const int seg = FB * (A.s_steps > 0 ? A.s_steps : 1);  // frames per piece
+  while (cu.b < A.batch) {
+    const int b = cu.b;
+    const int L = __builtin_amdgcn_readfirstlane(utt_len(A, b));
     const int T = (L + H - 1) / H + 1;
-    const int nstep = (T + FB - 1) / FB;
     rsrc_t r0, r1;
     rsrcs(b, r0, r1);
-    // the next utterance's first step is loaded during this one's last step (waves >= 1
-    // from inside the FFT, wave 0 right after it) and lands during the rescale
-    const int nb = next_valid(b + gridDim.x);
-    rsrc_t n0 = r_none, n1 = r_none;
-    if (nb < A.batch) rsrcs(nb, n0, n1);
+    // the next unit's first step is loaded during this unit's last step (waves >= 1 from
+    // inside the FFT, wave 0 right after it) and lands during the rescale (the next unit is
+    // looked up again after the loop: held across the steps it spilled)
+    int nb = 0, nlen = 0, nf0 = 0;  // the next unit's utterance, length (0: none), 1st frame
+    {
+      const Unit t = unit_at(cu.g + gridDim.x);
+      if (t.b < A.batch) {
+        nb = __builtin_amdgcn_readfirstlane(t.b);
+        nlen = __builtin_amdgcn_readfirstlane(utt_len(A, t.b));
+        nf0 = PIECES ? __builtin_amdgcn_readfirstlane(t.s_lo * FB) : 0;
+      }
+    }
     // the utterance's apply coefficients into LDS (read per step, so they hold no registers
-    // through the FFTs); the previous utterance's readers finished at its last barrier
+    // through the FFTs); the previous unit's readers finished at its last barrier. A piece
+    // reads the solve kernel's (the host launches it for the piece utterances).
     {
       float4* ct = reinterpret_cast<float4*>(lds + UttGeo::COEF_OFF);
-      if constexpr (SOLVE) {
+      if (SOLVE && (!PIECES || b < s_whole)) {
         const int nch = (T + kChunk - 1) / kChunk;
         for (int k = tid; k < F; k += kUttThreads) {
           double R[5], w[4];
@@ -1467,7 +1568,9 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         }
       } else {
         const float4* coef = reinterpret_cast<const float4*>(A.coef) + (long long)b * F;
-        for (int k = tid; k < F; k += kUttThreads) ct[k] = coef[k];
+        int k0 = tid;
+        opaque_i(k0);  // its address computed here (hoisted to the kernel start, it spilled)
+        for (int k = k0; k < F; k += kUttThreads) ct[k] = coef[k];
       }
     }
     __syncthreads();
@@ -1476,7 +1579,9 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     float4 carry = make_float4(0.f, 0.f, 0.f, 0.f);
     float peak = 0.0f;
     float* outb = A.out + (long long)b * A.out_stride;
-    for (int step = 0; step < nstep; ++step) {
+    const int s_hi = cu.s_hi, s_lo = PIECES ? cu.s_lo : 0;
+    int step = s_lo;
+    for (; step < s_hi; ++step) {
 #ifdef AVZ_STAMPS
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       AVZ_STAMP(13);
@@ -1487,7 +1592,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       int ln = lane, tq = tid;
       opaque_i(ln);
       opaque_i(tq);
-      if (f0 % kChunk == 0 && PF == PF_IBM_TARGET) {  // the chunk's post-filter bits
+      if ((f0 % kChunk == 0 || (PIECES && step == s_lo)) && PF == PF_IBM_TARGET) {  // bits
         const uint32_t* MW = A.mwords + ((long long)b * A.nchunk + c) * F;
 #pragma unroll
         for (int q = 0; q < 9; ++q)
@@ -1495,11 +1600,19 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       }
       // ---- window + forward FFT of frames f0 + 2 wave + g into slot my; the next step's
       // loads go out from inside its last stage (frames >= FB: no negative sample index)
-      const bool more = step + 1 < nstep;
-      const bool il = more || wave >= 1;
-      const rsrc_t q0 = more ? r0 : (wave >= 1 ? n0 : r_none);
-      const rsrc_t q1 = more ? r1 : (wave >= 1 ? n1 : r_none);
-      const int sn = ((more ? f0 + FB : 0) + my) * H - N / 2 + lm.in0;
+      const bool more = step + 1 < s_hi;
+      const bool il = more || wave >= 1 || nf0 > 0;
+      // the descriptors of the next step's loads, built from block-uniform scalars (a
+      // select between two descriptors went to VGPRs: a waterfall loop around every load)
+      rsrc_t q0, q1;
+      {
+        const int qb = __builtin_amdgcn_readfirstlane(more ? b : nb);
+        const int ql = __builtin_amdgcn_readfirstlane(more ? L : nlen);
+        const float* qm = A.mix + (long long)qb * A.mix_stride;
+        q0 = make_rsrc(qm, ql);
+        q1 = make_rsrc(qm + A.ch_stride, ql);
+      }
+      const int sn = ((more ? f0 + FB : nf0) + my) * H - N / 2 + lm.in0;
       // the next step's loads go out after the apply (issued from inside the forward FFT's
       // last stage, after the FFT or after the inverse measured slower)
       auto next_loads = [&]() {
@@ -1509,7 +1622,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
             v[k].y = bload_nn(q1, sn + 32 * k);
           });
         } else {
-          first_loads(n0, n1);  // wave 0, last step: the next utterance (or empty)
+          first_loads(q0, q1, 0);  // wave 0, last step: the next utterance (or empty)
         }
       };
       window_fft<N>(v, wc0, fft, utt_frame(lds, my), lm);
@@ -1607,6 +1720,9 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         return reinterpret_cast<const float*>(utt_frame(lds, f));
       };
       const int m0 = 4 * (tq & 127), sgrp = __builtin_amdgcn_readfirstlane(tq >> 7);
+      // a piece's first step (its first segment is a seam) and the piece's seam slot
+      const bool pstart = PIECES && b >= s_whole && f0 % seg == 0;
+      const long long pslot = (long long)(b - s_whole) * pieces + f0 / seg;
       auto ola = [&]() {
 #pragma unroll
       for (int si = 0; si < 4; ++si) {
@@ -1614,6 +1730,10 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         const int j = f0 - 1 + s;
         if (j >= 0 && j <= T - 2) {
           const float4 vb = *reinterpret_cast<const float4*>(cframe(s) + m0);
+          if (s == 0 && pstart) {  // a piece's first segment is a seam: its half for the
+            *reinterpret_cast<float4*>(A.pheads + pslot * H + m0) = vb;  // piece finalize
+            continue;
+          }
           // the previous frame's half read unconditionally (frame 0's when s = 0) and the
           // carry selected by value: a conditional read was split into four ds_read_b32
           // (4-way bank conflicts, 15 % of the kernel's LDS cycles), a pointer select with
@@ -1631,13 +1751,23 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       }
       };
       if (rs_out != nullptr && rs_done < rs_n4) {  // a slice of the previous utterance's rescale
-        const int lo = rs_done, hi = min(rs_n4, rs_done + RS_U * kUttThreads);
-        rescale_slice(std::integral_constant<int, RS_U>{}, lo, hi, ola);
-        rs_done = hi;
+        if (PIECES && b >= s_whole) {  // a piece's few steps: larger slices
+          const int lo = rs_done, hi = min(rs_n4, rs_done + RS_UP * kUttThreads);
+          rescale_slice(std::integral_constant<int, RS_UP>{}, lo, hi, ola);
+          rs_done = hi;
+        } else {
+          const int lo = rs_done, hi = min(rs_n4, rs_done + RS_U * kUttThreads);
+          rescale_slice(std::integral_constant<int, RS_U>{}, lo, hi, ola);
+          rs_done = hi;
+        }
       } else {
         ola();
       }
       if (sgrp == 0) carry = *reinterpret_cast<const float4*>(cframe(FB - 1) + H + m0);
+      // a piece's last half-frame (seam half): a whole utterance's last step never has a
+      // segment f0 + FB - 1 <= T - 2 (its last frame is T - 1 <= f0 + FB - 1)
+      if (PIECES && sgrp == 0 && !more && f0 + FB - 1 <= T - 2)
+        *reinterpret_cast<float4*>(A.ptails + pslot * H + m0) = carry;
       AVZ_STAMP(9);
       lds_barrier();
       AVZ_STAMP(10);
@@ -1651,8 +1781,13 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     float pk = red[0];
 #pragma unroll
     for (int w = 1; w < kUttThreads / 64; ++w) pk = fmaxf(pk, red[w]);
-    if (tid == 0 && A.peak) A.peak[b] = pk;
-    if (A.normalize == NORM_PEAK) {
+    const bool whole = !PIECES || b < s_whole;
+    if (!whole) {  // a piece: its interior's max (non-negative floats order as uints)
+      if (tid == 0) atomicMax(A.peak_u + b, __float_as_uint(pk));
+    } else if (tid == 0 && A.peak) {
+      A.peak[b] = pk;
+    }
+    if (whole && A.normalize == NORM_PEAK) {
       // the previous one's slices left over (an utterance of < 8 steps)
       if (rs_out != nullptr) rescale_rest(std::integral_constant<int, 2 * RS_U>{});
       rs_out = outb;
@@ -1660,9 +1795,11 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       rs_n4 = (T - 1) * H / 4;
       rs_done = 0;
     }
-    __syncthreads();  // red[] of the next utterance
+    __syncthreads();  // red[] of the next unit
     AVZ_STAMP(14);
-    b = nb;
+    // this unit's index: b (whole) or s_whole + the piece's, (step - 1) / s_steps its piece
+    cu = unit_at((whole ? b : s_whole + (b - s_whole) * pieces + (step - 1) / A.s_steps) +
+                 gridDim.x);
   }
   // the block's last utterance, after the loop where the sample registers are dead: every
   // load of a 4-s utterance in flight at once (the single-utterance blocks of B <= #CU
@@ -1738,8 +1875,9 @@ __global__ void __launch_bounds__(kUtt512Threads, 2) avz_synthesis_utt512_kernel
     return bb;
   };
   auto rsrcs = [&](int bb, rsrc_t& a0, rsrc_t& a1) {
+    bb = __builtin_amdgcn_readfirstlane(bb);
     const float* mixb = A.mix + (long long)bb * A.mix_stride;
-    const int len = utt_len(A, bb);
+    const int len = __builtin_amdgcn_readfirstlane(utt_len(A, bb));
     a0 = make_rsrc(mixb, len);
     a1 = make_rsrc(mixb + A.ch_stride, len);
   };
@@ -1996,9 +2134,8 @@ __global__ void __launch_bounds__(kUtt512Threads, 2) avz_synthesis_utt512_kernel
 template <int N>
 constexpr int kFinChunks = N >= 1024 ? 1 : 1024 / N;
 
-// One finalize item: chunks FCH q .. FCH q + FCH - 1 of utterance b — the standalone
-// finalize kernel's block, or a finalize item run inside the next synthesis launch (red:
-// NWAVE floats of LDS).
+// One finalize item: chunks FCH q .. FCH q + FCH - 1 of utterance b, the standalone
+// finalize kernel's block (red: NWAVE floats of LDS).
 template <int N>
 __device__ __forceinline__ void finalize_item(const ChainArgs& A, int q, int b, float* red) {
   constexpr int NT = kCThreads, H = N / 2, NWAVE = NT / 64, FCH = kFinChunks<N>;
@@ -2103,6 +2240,83 @@ __global__ void __launch_bounds__(kCThreads) avz_finalize_kernel(ChainArgs A) {
   finalize_item<N>(A, blockIdx.x, blockIdx.y, red);
 }
 
+// Finalize of the per-utterance synthesis kernel's piece utterances b = s_whole + blockIdx.y
+// (peak normalisation): the seam segments between its pieces (piece p - 1's last half-frame
+// + piece p's first, x 1 / sum w^2), the utterance peak (the pieces' interior maxima in
+// peak_u[b] and the seams), peak[b], and the in-place rescale of segments [0, T - 2], block x
+// taking kFinPieceU float4 groups per thread of them (every block reduces the few seams
+// itself: no cross-block hand-off).
+constexpr int kFinPieceU = 4;
+constexpr int kMaxPieces = 32;  // pieces per utterance (synth_split; avz_capi.cpp seam_slots)
+template <int N>
+__global__ void __launch_bounds__(kCThreads) avz_finalize_pieces_kernel(ChainArgs A) {
+  constexpr int H = N / 2, NWAVE = kCThreads / 64, FBS = UttGeo::FB;
+  __shared__ float red[NWAVE];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int b = A.s_whole + blockIdx.y;
+  const int L = utt_len(A, b);
+  if (L < N) {
+    if (blockIdx.x == 0 && tid == 0 && A.peak) A.peak[b] = __builtin_nanf("");
+    return;
+  }
+  const int T = (L + H - 1) / H + 1;
+  const int seg = FBS * A.s_steps;               // frames per piece
+  const int n4 = (T - 1) * H / 4;                // float4 groups of segments 0 .. T - 2
+  const int g0 = blockIdx.x * kFinPieceU * kCThreads;
+  if (g0 >= n4) return;
+  const long long slot0 = (long long)(b - A.s_whole) * A.s_pieces;
+  // seam segment j = p seg - 1 (p >= 1, j <= T - 2): tail of piece p - 1 + head of piece p
+  auto seam = [&](int p, int m) -> float {
+    return (A.ptails[(slot0 + p - 1) * H + m] + A.pheads[(slot0 + p) * H + m]) * inv_wsum<N>(m);
+  };
+  const int n_seam = (T - 2 + 1) / seg;          // p = 1 .. n_seam
+  const uint32_t pk_int = A.peak_u[b];  // the pieces' interior maxima (loaded with the rest)
+  float4 x[kFinPieceU];
+  float* outb = A.out + (long long)b * A.out_stride;
+  const float4* o4 = reinterpret_cast<const float4*>(outb);
+#pragma unroll
+  for (int u = 0; u < kFinPieceU; ++u) {
+    const int i = g0 + u * kCThreads + tid;
+    if (i < n4) x[u] = o4[i];                    // interior values stream while the seams reduce
+  }
+  // the seams' max: up to 7 seams x H values with all of a thread's loads in flight (more
+  // registers for the 31 seams of 32 pieces ran 10.5 -> 17 us at B = 257: 7 seams)
+  constexpr int SU = 7 * H / kCThreads;
+  float sv[SU];
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const int idx = tid + u * kCThreads;
+    sv[u] = idx < n_seam * H ? seam(idx / H + 1, idx % H) : 0.0f;
+  }
+  float pk = 0.0f;
+#pragma unroll
+  for (int u = 0; u < SU; ++u) pk = fmaxf(pk, fabsf(sv[u]));
+  for (int idx = tid + SU * kCThreads; idx < n_seam * H; idx += kCThreads)  // more (not split
+    pk = fmaxf(pk, fabsf(seam(idx / H + 1, idx % H)));                      // so finely)
+  for (int o = 32; o > 0; o >>= 1) pk = fmaxf(pk, __shfl_xor(pk, o, 64));
+  if (lane == 0) red[wave] = pk;
+  __syncthreads();
+  pk = __uint_as_float(pk_int);
+#pragma unroll
+  for (int w = 0; w < NWAVE; ++w) pk = fmaxf(pk, red[w]);
+  if (blockIdx.x == 0 && tid == 0 && A.peak) A.peak[b] = pk;
+  const float scale = 1.0f / (pk + A.norm_eps);
+  float4* w4 = reinterpret_cast<float4*>(outb);
+#pragma unroll
+  for (int u = 0; u < kFinPieceU; ++u) {
+    const int i = g0 + u * kCThreads + tid;
+    if (i >= n4) continue;
+    const int j = 4 * i / H, m = 4 * i % H;
+    float4 y = x[u];
+    if ((j + 1) % seg == 0) {                    // a seam (j = p seg - 1 <= T - 2)
+      const int p = (j + 1) / seg;
+      y = make_float4(seam(p, m), seam(p, m + 1), seam(p, m + 2), seam(p, m + 3));
+    }
+    y.x *= scale; y.y *= scale; y.z *= scale; y.w *= scale;
+    w4[i] = y;
+  }
+}
+
 // Grid x of the finalize kernel: FCH-chunk groups of the longest utterance.
 template <int N>
 static inline int fin_groups(int nch) { return (nch + kFinChunks<N> - 1) / kFinChunks<N>; }
@@ -2130,10 +2344,14 @@ extern "C" int avz_debug_set_synth_variant(int v) {
 // chunk grid + finalize. It pays for peak normalisation only (the rescale folded in, no
 // finalize launch); without it the chunk grid's synthesis + seam pass is the faster pair
 // (B = 256: 70.7 + 4.2 vs 79.9 us, profiles/r04/ab_synth_utt.txt).
+// At N = 512 (no piece split there) only whole rounds take it: a partial round, or a batch
+// below the CU count, runs the chunk grid + finalize (at B = 1 the 8.23-s test triple's 17
+// per-utterance steps on one CU took 154 us of synthesis).
 template <int N, int PF, bool SPEC>
 static bool synth_per_utterance(const ChainArgs* a) {
-  return (N == 1024 || N == 512) && !SPEC && (PF == PF_IBM_TARGET || PF == PF_NONE) &&
-         a->normalize == NORM_PEAK && g_synth_variant.load(std::memory_order_relaxed) >= 1;
+  return (N == 1024 || (N == 512 && a->batch % resident_cus() == 0)) && !SPEC &&
+         (PF == PF_IBM_TARGET || PF == PF_NONE) && a->normalize == NORM_PEAK &&
+         g_synth_variant.load(std::memory_order_relaxed) >= 1;
 }
 // ... and solves the utterance's bins itself (variant 2) when the chain's solve is the plain
 // MVDR one: no item-level fallback flags, no covariance / weight debug outputs.
@@ -2144,24 +2362,93 @@ static bool solve_fused(const ChainArgs* a) {
          !a->cov_only;
 }
 
+// Work split of the N = 1024 per-utterance synthesis (ChainArgs s_whole / s_pieces /
+// s_steps): with R resident blocks (one per CU), whole utterances for the full rounds
+// floor(B / R) R, and the partial last round's rem utterances -- or a whole batch below R --
+// in pieces of s_steps steps (16 frames each) spread over the grid, when that is cheaper than
+// one more round of whole utterances. Cost model in steps of the kernel (~9.5 us at two waves
+// per SIMD): a whole round S steps + 2 (the in-block solve and the exposed rescale of its
+// last utterance); pieces ceil(rem pu / R) s_steps + 2 (the pieces' solve and finalize
+// launches, ~10 us each with their kernel boundaries) + 2 rem / R (the finalize's rescale
+// traffic).
+struct SynthSplit {
+  int whole, pieces, steps, grid;
+};
+static SynthSplit synth_split(const ChainArgs* a) {
+  constexpr int FB = UttGeo::FB;
+  const int R = resident_cus(), B = a->batch;
+  const int S = (a->max_frames + FB - 1) / FB;  // steps of the longest utterance
+  const SynthSplit all_whole{B, 0, S, std::min(B, R)};
+  if (!a->pheads || !a->ptails || B <= 0) return all_whole;
+  const int full = B / R, rem = B - full * R;
+  if (rem == 0) return all_whole;
+  int pu = std::min(kMaxPieces, std::min(S, std::max(1, R / rem)));
+  pu = std::min(pu, a->pseam_slots / rem);
+  if (pu < 1) return all_whole;
+  const int sp = (S + pu - 1) / pu;
+  pu = (S + sp - 1) / sp;
+  const long long units = (long long)rem * pu;
+  const long long rounds = (units + R - 1) / R;
+  const double c_whole = S + 2.0, c_piece = (double)rounds * sp + 2.0 + 2.0 * rem / R;
+  if (c_piece >= c_whole) return all_whole;
+  return SynthSplit{full * R, pu, sp, full > 0 ? R : (int)std::min<long long>(units, R)};
+}
+
 // Synthesis + output normalisation of the chain and of the stage exports: the per-utterance
-// kernel (N = 1024, time-domain input; finalize events record an empty span), or the
-// persistent chunk grid followed by avz_finalize_kernel.
+// kernel (time-domain input, peak normalisation; finalize events record an empty span unless
+// the N = 1024 split has pieces, whose solve and finalize launches the solve and finalize
+// events then time), or the persistent chunk grid followed by avz_finalize_kernel. ev: the
+// (start, stop) event pairs of the solve, synthesis and finalize launches (6, may be null).
 template <int N, int PF, bool SPEC = false>
 static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
 template <int N, int PF, bool SPEC = false>
-static int launch_synth_finalize(const ChainArgs* a, hipStream_t st, hipEvent_t e0, hipEvent_t e1,
-                                 hipEvent_t e2, hipEvent_t e3, bool fused_solve = false) {
+static int launch_synth_finalize(const ChainArgs* a0, hipStream_t st, const hipEvent_t* ev,
+                                 bool fused_solve = false) {
+  ChainArgs c = *a0;
+  const ChainArgs* a = &c;
+  auto evt = [&](int i) -> hipEvent_t { return ev ? ev[i] : nullptr; };
+  const hipEvent_t e0 = evt(2), e1 = evt(3), e2 = evt(4), e3 = evt(5);
   if (synth_per_utterance<N, PF, SPEC>(a)) {
     constexpr int UPF = (PF == PF_IBM_TARGET || PF == PF_NONE) ? PF : PF_NONE;  // instantiated
-    const dim3 grid((unsigned)std::min(a->batch, resident_cus()));
+    dim3 grid((unsigned)std::min(a->batch, resident_cus()));
+    c.s_whole = a->batch;
+    c.s_pieces = 0;
+    if constexpr (N == 1024) {
+      const SynthSplit sp = synth_split(a);
+      c.s_whole = sp.whole;
+      c.s_pieces = sp.pieces;
+      c.s_steps = sp.steps;
+      grid = dim3((unsigned)sp.grid);
+      if (sp.pieces > 0 && fused_solve) {  // the pieces' coefficients: the solve kernel's
+        ChainArgs s = c;
+        s.b_lo = sp.whole;
+        const int n = (int)(((long long)(a->batch - sp.whole) * (N / 2 + 1) + kSolveThreads - 1) /
+                            kSolveThreads);
+        hipExtLaunchKernelGGL(avz_solve_kernel<N>, dim3(n), dim3(kSolveThreads), 0, st, evt(0),
+                              evt(1), 0, s);
+      }
+    }
     if constexpr (N == 1024) {
       constexpr int lds = UttGeo::LDS_BYTES;
-      auto kern = fused_solve ? avz_synthesis_utt_kernel<UPF, true> : avz_synthesis_utt_kernel<UPF, false>;
-      if (!(fused_solve ? lds_ready<avz_synthesis_utt_kernel<UPF, true>>(lds)
-                        : lds_ready<avz_synthesis_utt_kernel<UPF, false>>(lds)))
-        return -3;
+      const bool pc = c.s_pieces > 0;
+      auto kern = fused_solve ? (pc ? avz_synthesis_utt_kernel<UPF, true, true>
+                                    : avz_synthesis_utt_kernel<UPF, true, false>)
+                              : (pc ? avz_synthesis_utt_kernel<UPF, false, true>
+                                    : avz_synthesis_utt_kernel<UPF, false, false>);
+      const bool ready = fused_solve
+                             ? (pc ? lds_ready<avz_synthesis_utt_kernel<UPF, true, true>>(lds)
+                                   : lds_ready<avz_synthesis_utt_kernel<UPF, true, false>>(lds))
+                             : (pc ? lds_ready<avz_synthesis_utt_kernel<UPF, false, true>>(lds)
+                                   : lds_ready<avz_synthesis_utt_kernel<UPF, false, false>>(lds));
+      if (!ready) return -3;
       hipExtLaunchKernelGGL(kern, grid, dim3(kUttThreads), lds, st, e0, e1, 0, *a);
+      if (c.s_pieces > 0) {
+        const int T = a->max_frames;
+        const int n4 = (T - 1) * (N / 2) / 4;
+        const int gx = (n4 + kFinPieceU * kCThreads - 1) / (kFinPieceU * kCThreads);
+        hipExtLaunchKernelGGL(avz_finalize_pieces_kernel<N>, dim3(gx, a->batch - c.s_whole),
+                              dim3(kCThreads), 0, st, e2, e3, 0, *a);
+      }
     } else {
       constexpr int lds = Utt512Geo::LDS_BYTES;
       auto kern = fused_solve ? avz_synthesis_utt512_kernel<UPF, true>
@@ -2171,9 +2458,7 @@ static int launch_synth_finalize(const ChainArgs* a, hipStream_t st, hipEvent_t 
         return -3;
       hipExtLaunchKernelGGL(kern, grid, dim3(kUtt512Threads), lds, st, e0, e1, 0, *a);
     }
-    (void)e2;  // no finalize launch: its events stay unrecorded (avz_chain_kernels)
-    (void)e3;
-    return 0;
+    return 0;  // no finalize launch unless pieces: its events stay unrecorded (avz_chain_kernels)
   }
   if (launch_synthesis<N, PF, SPEC>(a, st, e0, e1) != 0) return -3;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
@@ -2215,17 +2500,42 @@ static int resident_cus() {
   return v;
 }
 
+// Tail splitting of the analysis grid (analysis_items): with G resident blocks, the
+// floor(n / G) G items of the full rounds run whole and the partial last round's items in
+// P step-range pieces each (P <= SA, the steps of a chunk; P * tail <= G, the tail slots), so
+// that round takes 1/P of an item's time instead of a whole one (B = 257: 1028 items over
+// 512 blocks ran a third round of 4 items). Returns the grid.
+static int analysis_tail(ChainArgs& c, int n_items, int G, int SA) {
+  c.a_whole = n_items;
+  c.a_pieces = 1;
+  const int whole = n_items / G * G, tail = n_items - whole;
+  int P = 1;
+  if (tail > 0 && c.tpart != nullptr)
+    for (int q = SA; q >= 2; q >>= 1)
+      if ((long long)tail * q <= G && (long long)tail * q <= c.tpart_slots) {
+        P = q;
+        break;
+      }
+  if (P == 1) return std::min(n_items, G);
+  c.a_whole = whole;
+  c.a_pieces = P;
+  return whole > 0 ? G : tail * P;
+}
+
 template <int N, int MASK, int PF>
-static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
+static int launch_chunked_t(const ChainArgs* a0, hipStream_t st) {
   auto k1 = avz_analysis_kernel<N, MASK, PF == PF_IRM>;
   auto k3 = avz_finalize_kernel<N>;
   auto ks = avz_solve_kernel<N>;
   constexpr int lds = CGeo<N>::LDS_BYTES;
   if (!lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM>>(lds)) return -3;
+  ChainArgs c = *a0;  // this launch's copy (tail splitting parameters)
+  const ChainArgs* a = &c;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
   const int n_items = nch * a->batch;
-  const dim3 pgrid((unsigned)std::min(n_items, CGeo<N>::BLOCKS * resident_cus()));
+  constexpr int SA = kChunk / ((MASK == MASK_IBM) ? CGeo<N>::NSLOT / 2 : CGeo<N>::NSLOT);
+  const dim3 pgrid((unsigned)analysis_tail(c, n_items, CGeo<N>::BLOCKS * resident_cus(), SA));
   constexpr int F = N / 2 + 1;
   const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
   // diagnostic timing: kernel i's (start, stop) events ride on its own dispatch packet
@@ -2246,7 +2556,8 @@ static int launch_chunked_t(const ChainArgs* a, hipStream_t st) {
     hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), evt(3), 0, *a);
   }
   (void)k3;
-  if (launch_synth_finalize<N, PF>(a, st, evt(4), evt(5), evt(6), evt(7), fused) != 0) return -3;
+  const hipEvent_t sev[6] = {evt(2), evt(3), evt(4), evt(5), evt(6), evt(7)};
+  if (launch_synth_finalize<N, PF>(a, st, sev, fused) != 0) return -3;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -2299,7 +2610,9 @@ extern "C" int avz_chain_kernels(int n_fft, const ChainArgs* a) {
   bool utt = false, fused = false;
   if (n_fft == 1024) chain_kernels_t<1024>(a, utt, fused);
   if (n_fft == 512) chain_kernels_t<512>(a, utt, fused);
-  return 1 | (fused ? 0 : 2) | 4 | (utt ? 0 : 8);
+  // the N = 1024 per-utterance kernel's pieces bring a solve (fused plans) and a finalize
+  const bool pieces = utt && n_fft == 1024 && synth_split(a).pieces > 0;
+  return 1 | (fused && !pieces ? 0 : 2) | 4 | (utt && !pieces ? 0 : 8);
 }
 
 extern "C" int avz_launch_chunked(int n_fft, int mask_mode, const ChainArgs* a, void* stream) {
@@ -2344,8 +2657,10 @@ static int launch_cov_t(const ChainArgs* a, hipStream_t st) {
   const int n_items = nch * a->batch;
   ChainArgs c = *a;
   c.cov_only = 1;
-  hipLaunchKernelGGL((avz_analysis_kernel<N, MASK, false>),
-                     dim3((unsigned)std::min(n_items, CGeo<N>::BLOCKS * resident_cus())),
+  // the chain's tail splitting, so the sums equal the fused call's bitwise
+  constexpr int SA = kChunk / ((MASK == MASK_IBM) ? CGeo<N>::NSLOT / 2 : CGeo<N>::NSLOT);
+  const int grid = analysis_tail(c, n_items, CGeo<N>::BLOCKS * resident_cus(), SA);
+  hipLaunchKernelGGL((avz_analysis_kernel<N, MASK, false>), dim3((unsigned)grid),
                      dim3(kCThreads), lds, st, c);
   constexpr int F = N / 2 + 1;
   const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
@@ -2378,7 +2693,7 @@ static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
   if (a->peak && a->normalize != NORM_PEAK &&
       hipMemsetAsync(a->peak, 0, sizeof(float) * a->batch, st) != hipSuccess)
     return -3;
-  if (launch_synth_finalize<N, PF, SPEC>(a, st, nullptr, nullptr, nullptr, nullptr) != 0) return -3;
+  if (launch_synth_finalize<N, PF, SPEC>(a, st, nullptr) != 0) return -3;
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

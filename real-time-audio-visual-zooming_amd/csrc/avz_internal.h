@@ -54,6 +54,22 @@ struct ChainArgs {
   int spec_frames;            // frames present in S (frames >= spec_frames read as zero)
   int cov_only;               // solve kernel: write cov_out only (the covariance stage export)
   int* flag;                  // [B] item-level (batch_mvdr) fallback flags, zeroed per call
+  // Tail splitting of the persistent grids (set per launch by the launcher; zero = off).
+  // Analysis: items [0, a_whole) run whole, each later (chunk, utterance) item in a_pieces
+  // step-range pieces whose partials go to tpart[(item - a_whole) * a_pieces + p][5][F]
+  // (the solve sums them in fp64) and whose IBM bits are merged into mwords atomically.
+  int a_whole, a_pieces;
+  float* tpart;               // [tpart_slots][5][F]
+  int tpart_slots;
+  // Per-utterance synthesis: utterances [0, s_whole) whole (in-block seams, peak, rescale),
+  // utterances [s_whole, batch) in s_pieces pieces of s_steps steps each, whose boundary
+  // half-frames go to pheads / ptails[(b - s_whole) * s_pieces + p][H] for the piece
+  // finalize kernel (seams, peak, rescale).
+  int s_whole, s_pieces, s_steps;
+  float* pheads;
+  float* ptails;
+  int pseam_slots;
+  int b_lo;                   // solve / piece-finalize launches: first utterance
   void* const* events;        // host-only: (start, stop) hipEvent_t pairs of the 4 launches, or null
   int n_events;               // host-only: how many of them to use (8, or 2: analysis only)
 };

@@ -136,8 +136,10 @@ def test_plan_timing_modes(gpu_device):
     """avz_plan_set_timing: mode 1 times all four kernels, mode 2 the analysis kernel
     only (NaN for the rest), 0 turns it off (get_timing then reports an argument error).
     With peak normalisation at N = 1024 the per-utterance synthesis kernel folds finalize
-    (and, for plain MVDR plans, the solve) in, which then count 0; without it
-    (normalize="none") all four kernels run and are timed."""
+    (and, for plain MVDR plans, the solve) in, which then count 0 -- unless, as for this
+    batch of 4 (below the CU count), it splits the utterances into step pieces, which
+    launch a solve and a piece finalize; without peak normalisation (normalize="none") all
+    four kernels run and are timed."""
     import math
 
     import avz
@@ -154,8 +156,8 @@ def test_plan_timing_modes(gpu_device):
         t = plan.timing()
         assert t["calls"] == 3 and t["analysis"] > 0
         others = [t[k] for k in ("solve", "synthesis", "finalize")]
-        if mode == "all":
-            assert others[1] > 0 and others[2] == 0.0 and others[0] >= 0.0
+        if mode == "all":  # B = 4 < #CU: split into pieces, whose solve and finalize run
+            assert others[0] > 0 and others[1] > 0 and others[2] > 0
         else:
             assert all(math.isnan(v) for v in others)
     plan_n = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",

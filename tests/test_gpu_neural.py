@@ -110,3 +110,25 @@ def test_main_deploy_file_mirror(neural, gpu_device, tmp_path, monkeypatch):
     ref = golden("neural_excerpt_test.npz")["out"]
     assert np.max(np.abs(out - ref)) <= WAVE_TOL
     assert N.main_deploy(str(tmp_path / "input.wav"), model_path=str(tmp_path / "absent.pth")) is None
+
+
+def test_refresh_after_weight_change(neural, gpu_device):
+    """fold_bn snapshots the caller's weights (a BatchNorm-folded copy): a later change to
+    the caller's model is not seen until refresh(model) rebuilds the copy."""
+    import copy
+    N, model0 = neural
+    model = copy.deepcopy(model0)
+    bf = N.NeuralMaskBeamformer(model, max_items=2)
+    x = torch.randn((2, 2, 16000), device=gpu_device)
+    items = bf.split(x)[0]
+    m0 = bf.masks(items).clone()
+    with torch.no_grad():
+        for p in model.parameters():
+            p.mul_(1.5)
+    torch.testing.assert_close(bf.masks(items), m0, rtol=0, atol=0)  # the snapshot
+    bf.refresh(model)
+    m1 = bf.masks(items)
+    with torch.no_grad():
+        ref = model(N.mask_features(bf.plan, items, "unet"))
+    assert not torch.equal(m1, m0)
+    torch.testing.assert_close(m1, ref, rtol=1e-4, atol=1e-5)
