@@ -747,16 +747,16 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
 
 // The block's work units: whole items i, i + gridDim.x, ... below a_whole (a multiple of the
 // grid), then the tail items' pieces on the same stride (tail splitting, ChainArgs).
-template <int N, int MASK, bool IRM, class TW>
+template <int N, int MASK, bool IRM, bool SPLIT, class TW>
 __device__ __forceinline__ void analysis_items(const ChainArgs& A, unsigned char* lds, int gx,
                                                int n_items, const TW& tw_reg,
                                                const LaneConst<N>& K) {
-  const int P = A.a_pieces > 1 ? A.a_pieces : 1;
+  const int P = SPLIT && A.a_pieces > 1 ? A.a_pieces : 1;
   const int n_whole = P > 1 ? A.a_whole : n_items;
   int u = blockIdx.x;
   for (; u < n_whole; u += gridDim.x)
     analysis_item<N, MASK, IRM>(A, lds, u % gx, u / gx, 0, 1, -1, tw_reg, K);
-  if (P > 1) {
+  if (SPLIT && P > 1) {
     const int n_units = (n_items - n_whole) * P;
     for (int q = u - n_whole; q < n_units; q += gridDim.x) {
       const int it = n_whole + q / P;
@@ -768,8 +768,10 @@ __device__ __forceinline__ void analysis_items(const ChainArgs& A, unsigned char
 // Persistent grid (about two blocks per CU): block i takes the (chunk, utterance) items
 // i, i + gridDim.x, ... so the twiddle table is built once per block and the batch is
 // spread evenly over the resident blocks (no second, partly idle round of short blocks);
-// a partial last round is split into step-range pieces (analysis_items).
-template <int N, int MASK, bool IRM>
+// a partial last round is split into step-range pieces (analysis_items; the SPLIT instance,
+// launched only when the tail splitting is on, so the whole-rounds instance carries none of
+// its code).
+template <int N, int MASK, bool IRM, bool SPLIT = false>
 __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysis_kernel(ChainArgs A) {
   using G = CGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -787,11 +789,11 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysi
     }
     LaneConst<N> K;
     K.init(threadIdx.x);
-    analysis_items<N, MASK, IRM>(A, lds, gx, n_items, tw_reg, K);
+    analysis_items<N, MASK, IRM, SPLIT>(A, lds, gx, n_items, tw_reg, K);
   } else {
     LaneConst<N> K;
     K.init(threadIdx.x);
-    analysis_items<N, MASK, IRM>(A, lds, gx, n_items, NoTw{}, K);
+    analysis_items<N, MASK, IRM, SPLIT>(A, lds, gx, n_items, NoTw{}, K);
   }
 }
 
@@ -805,7 +807,7 @@ constexpr int kSolveThreads = 256;
 // by 1/4 (the analysis accumulates (2 y)(2 y)^H).
 // V: split-chunk partial vectors per round trip (the per-utterance kernels' fallback takes
 // few: its prefetched samples are live there).
-template <int N, int V = 8>
+template <int N, int V = 8, bool SPLIT = true>
 __device__ __forceinline__ void bin_cov_sums(const ChainArgs& A, int b, int k, int nch,
                                              double (&R)[5]) {
   constexpr int F = N / 2 + 1;
@@ -814,12 +816,13 @@ __device__ __forceinline__ void bin_cov_sums(const ChainArgs& A, int b, int k, i
   for (int q = 0; q < 5; ++q) R[q] = 0.0;
   // chunks of a split tail item (analysis_items) sum their pieces' partials
   const long long it0 = (long long)b * ((A.max_frames + kChunk - 1) / kChunk);
-  const int cw = A.a_pieces > 1 ? (int)max(0LL, min((long long)nch, A.a_whole - it0)) : nch;
+  const int cw =
+      SPLIT && A.a_pieces > 1 ? (int)max(0LL, min((long long)nch, A.a_whole - it0)) : nch;
   for (int cc = 0; cc < cw; ++cc) {
 #pragma unroll
     for (int q = 0; q < 5; ++q) R[q] += (double)P[((long long)cc * 5 + q) * F];
   }
-  if (cw < nch) {
+  if (SPLIT && cw < nch) {
     // the split chunks' pieces: (nch - cw) a_pieces consecutive partial vectors of tpart,
     // V per round trip through a descriptor covering exactly them (absent ones read +0,
     // which leaves the sums unchanged); summed in chunk and piece order
@@ -845,11 +848,11 @@ __device__ __forceinline__ void bin_cov_sums(const ChainArgs& A, int b, int k, i
 // partials of up to four chunks per round trip through a buffer descriptor covering
 // exactly the utterance's nch chunks, so the loads of absent chunks read +0 without
 // branches and the sums (chunk order kept, + 0 changes nothing) are bitwise those above.
-template <int N>
+template <int N, bool SPLIT = true>
 __device__ __forceinline__ void bin_cov_sums_utt(const ChainArgs& A, int b, int k, int nch,
                                                  double (&R)[5]) {
   constexpr int F = N / 2 + 1;
-  if (A.a_pieces > 1 &&
+  if (SPLIT && A.a_pieces > 1 &&
       (long long)b * ((A.max_frames + kChunk - 1) / kChunk) + nch > A.a_whole) {
     bin_cov_sums<N, 4>(A, b, k, nch, R);  // some of its chunks were split (block-uniform)
     return;
@@ -872,7 +875,7 @@ __device__ __forceinline__ void bin_cov_sums_utt(const ChainArgs& A, int b, int 
   for (int q = 0; q < 4; ++q) R[q] *= 0.25;
 }
 
-template <int N>
+template <int N, bool SPLIT = false>
 __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   constexpr int H = N / 2, F = N / 2 + 1;
   const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
@@ -883,7 +886,7 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
   double R[5];
-  bin_cov_sums<N>(A, b, k, nch, R);
+  bin_cov_sums<N, 8, SPLIT>(A, b, k, nch, R);
   if (A.cov_only) {  // covariance stage export
 #pragma unroll
     for (int q = 0; q < 5; ++q) A.cov_out[((long long)b * F + k) * 5 + q] = R[q];
@@ -1426,7 +1429,6 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
   float inv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(4 * (tid & 127) + i);
-  const rsrc_t r_none = make_rsrc(nullptr, 0);
   __syncthreads();  // twiddle table
   AVZ_STAMP_DECL();
   AVZ_STAMP_INIT();
@@ -1454,7 +1456,8 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         if (tid == 0 && A.peak) A.peak[g] = __builtin_nanf("");
         continue;
       }
-      const int q = g - s_whole, bq = s_whole + q / pieces, lo = (q % pieces) * A.s_steps;
+      const int pc = pieces > 0 ? pieces : 1;  // (0 only in the whole-rounds instance)
+      const int q = g - s_whole, bq = s_whole + q / pc, lo = (q % pc) * A.s_steps;
       const int Lq = __builtin_amdgcn_readfirstlane(utt_len(A, bq));
       const int ns = ((Lq + H - 1) / H + 1 + FB - 1) / FB;
       if (Lq >= N && lo < ns) return Unit{g, bq, lo, min(ns, lo + A.s_steps), q};
@@ -1559,7 +1562,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         const int nch = (T + kChunk - 1) / kChunk;
         for (int k = tid; k < F; k += kUttThreads) {
           double R[5], w[4];
-          bin_cov_sums_utt<N>(A, b, k, nch, R);
+          bin_cov_sums_utt<N, PIECES>(A, b, k, nch, R);
           const double* d = A.steer + 4 * k;
           mvdr_weights_d(R, k, N, A, d[0], d[1], d[2], d[3], w, nullptr);
           cf al, be;
@@ -2424,13 +2427,15 @@ static int launch_synth_finalize(const ChainArgs* a0, hipStream_t st, const hipE
         s.b_lo = sp.whole;
         const int n = (int)(((long long)(a->batch - sp.whole) * (N / 2 + 1) + kSolveThreads - 1) /
                             kSolveThreads);
-        hipExtLaunchKernelGGL(avz_solve_kernel<N>, dim3(n), dim3(kSolveThreads), 0, st, evt(0),
-                              evt(1), 0, s);
+        auto ks = c.a_pieces > 1 ? avz_solve_kernel<N, true> : avz_solve_kernel<N, false>;
+        hipExtLaunchKernelGGL(ks, dim3(n), dim3(kSolveThreads), 0, st, evt(0), evt(1), 0, s);
       }
     }
     if constexpr (N == 1024) {
       constexpr int lds = UttGeo::LDS_BYTES;
-      const bool pc = c.s_pieces > 0;
+      // the general instance for pieces and for split analysis chunks (the whole-rounds one
+      // reads only whole-chunk partials)
+      const bool pc = c.s_pieces > 0 || c.a_pieces > 1;
       auto kern = fused_solve ? (pc ? avz_synthesis_utt_kernel<UPF, true, true>
                                     : avz_synthesis_utt_kernel<UPF, true, false>)
                               : (pc ? avz_synthesis_utt_kernel<UPF, false, true>
@@ -2524,11 +2529,8 @@ static int analysis_tail(ChainArgs& c, int n_items, int G, int SA) {
 
 template <int N, int MASK, int PF>
 static int launch_chunked_t(const ChainArgs* a0, hipStream_t st) {
-  auto k1 = avz_analysis_kernel<N, MASK, PF == PF_IRM>;
   auto k3 = avz_finalize_kernel<N>;
-  auto ks = avz_solve_kernel<N>;
   constexpr int lds = CGeo<N>::LDS_BYTES;
-  if (!lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM>>(lds)) return -3;
   ChainArgs c = *a0;  // this launch's copy (tail splitting parameters)
   const ChainArgs* a = &c;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
@@ -2536,6 +2538,13 @@ static int launch_chunked_t(const ChainArgs* a0, hipStream_t st) {
   const int n_items = nch * a->batch;
   constexpr int SA = kChunk / ((MASK == MASK_IBM) ? CGeo<N>::NSLOT / 2 : CGeo<N>::NSLOT);
   const dim3 pgrid((unsigned)analysis_tail(c, n_items, CGeo<N>::BLOCKS * resident_cus(), SA));
+  const bool split = c.a_pieces > 1;  // the SPLIT instances only then
+  auto k1 = split ? avz_analysis_kernel<N, MASK, PF == PF_IRM, true>
+                  : avz_analysis_kernel<N, MASK, PF == PF_IRM, false>;
+  auto ks = split ? avz_solve_kernel<N, true> : avz_solve_kernel<N, false>;
+  if (!(split ? lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM, true>>(lds)
+              : lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM, false>>(lds)))
+    return -3;
   constexpr int F = N / 2 + 1;
   const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
   // diagnostic timing: kernel i's (start, stop) events ride on its own dispatch packet
@@ -2651,7 +2660,9 @@ __global__ void __launch_bounds__(256) avz_coef_kernel(ChainArgs A, const float*
 template <int N, int MASK>
 static int launch_cov_t(const ChainArgs* a, hipStream_t st) {
   constexpr int lds = CGeo<N>::LDS_BYTES;
-  if (!lds_ready<avz_analysis_kernel<N, MASK, false>>(lds)) return -3;
+  if (!lds_ready<avz_analysis_kernel<N, MASK, false, true>>(lds) ||
+      !lds_ready<avz_analysis_kernel<N, MASK, false, false>>(lds))
+    return -3;
   const int nch = (a->max_frames + kChunk - 1) / kChunk;
   if (nch > a->nchunk) return -2;
   const int n_items = nch * a->batch;
@@ -2660,11 +2671,14 @@ static int launch_cov_t(const ChainArgs* a, hipStream_t st) {
   // the chain's tail splitting, so the sums equal the fused call's bitwise
   constexpr int SA = kChunk / ((MASK == MASK_IBM) ? CGeo<N>::NSLOT / 2 : CGeo<N>::NSLOT);
   const int grid = analysis_tail(c, n_items, CGeo<N>::BLOCKS * resident_cus(), SA);
-  hipLaunchKernelGGL((avz_analysis_kernel<N, MASK, false>), dim3((unsigned)grid),
-                     dim3(kCThreads), lds, st, c);
+  const bool split = c.a_pieces > 1;
+  auto ka = split ? avz_analysis_kernel<N, MASK, false, true>
+                  : avz_analysis_kernel<N, MASK, false, false>;
+  auto ks = split ? avz_solve_kernel<N, true> : avz_solve_kernel<N, false>;
+  hipLaunchKernelGGL(ka, dim3((unsigned)grid), dim3(kCThreads), lds, st, c);
   constexpr int F = N / 2 + 1;
   const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
-  hipLaunchKernelGGL(avz_solve_kernel<N>, dim3(nsolve), dim3(kSolveThreads), 0, st, c);
+  hipLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, c);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
