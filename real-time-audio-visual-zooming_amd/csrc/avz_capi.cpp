@@ -30,6 +30,7 @@ struct Workspace {
   float* pheads;             // [seam_slots][H] per-utterance synthesis pieces' seam halves
   float* ptails;
   int seam_slots;
+  avz::PieceState* pstate;   // [batch] in-kernel piece finalize: arrivals, 1/peak, hand-backs
 };
 
 // Tail-splitting capacity (ChainArgs a_* / s_*): analysis pieces of a partial last round
@@ -74,8 +75,9 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
     w->pheads = reinterpret_cast<float*>(q); q += sz_seam;
     w->ptails = reinterpret_cast<float*>(q); q += sz_seam;
     w->seam_slots = ss;
+    w->pstate = reinterpret_cast<avz::PieceState*>(q); q += 4 * sz_b;
   }
-  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 2 * sz_b + sz_gain + sz_tpart + 2 * sz_seam;
+  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 6 * sz_b + sz_gain + sz_tpart + 2 * sz_seam;
 }
 
 struct avz_plan {
@@ -354,6 +356,7 @@ static int prepare_chain(const avz_plan* p, const avz_batch_args* a, int use, av
   k.pheads = ws.pheads;
   k.ptails = ws.ptails;
   k.pseam_slots = ws.seam_slots;
+  k.pstate = ws.pstate;
   if (use == USE_COVARIANCE) {  // that stage produces cov_out only: leave the caller's
     k.out = nullptr;            // out / peak / w buffers untouched (the analysis kernel
     k.peak = nullptr;           // would otherwise zero peak[b] as the atomicMax target)

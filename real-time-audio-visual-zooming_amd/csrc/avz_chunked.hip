@@ -284,8 +284,23 @@ __device__ __forceinline__ void pair_finish(cf (&v)[32]) {
 
 // Samples of utterance b: the device length clamped to the host-validated max_len (so an
 // inconsistent len[] never moves an access outside the caller's rows), or max_len for all.
+// A piece's seam half: written through to memory (agent-scope stores, sc1), so the last
+// piece of the utterance to arrive -- on any XCD -- reads it in the same kernel.
+// (row: block-uniform base of n floats; i: the thread's element)
+__device__ __forceinline__ void store_through(float* row, int n, int i, float4 v) {
+  const v4i_t d = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z),
+                   __float_as_int(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(d, make_rsrc(row, n), 4 * i, 0, kSC1);
+}
+
+// len[] is read-only for the whole chain, so it is read through the constant address space:
+// with a wave-uniform b that is one s_load_dword (scalar cache) instead of a vector load
+// plus readfirstlane on the item / unit start's dependent latency chain.
 __device__ __forceinline__ int utt_len(const ChainArgs& A, int b) {
-  return A.len ? min(A.len[b], A.max_len) : A.max_len;
+  if (!A.len) return A.max_len;
+  const __attribute__((address_space(4))) int* lc =
+      (const __attribute__((address_space(4))) int*)(A.len);
+  return min(lc[b], A.max_len);
 }
 
 // IBM decision |S_int| > |S_tgt| (oracle_debug.py:49-53, strict) from the packed reference
@@ -775,6 +790,10 @@ template <int N, int MASK, bool IRM, bool SPLIT = false>
 __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysis_kernel(ChainArgs A) {
   using G = CGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
+  // the per-utterance synthesis' piece finalize state, reset here (the next launch reads it)
+  if (A.pstate)
+    for (int b = blockIdx.x * kCThreads + threadIdx.x; b < A.batch; b += gridDim.x * kCThreads)
+      A.pstate[b] = PieceState{};
   KCfg<N>::Fft::fill_twiddles(reinterpret_cast<cf*>(lds + G::TW_OFF), threadIdx.x, G::NT);
   const int gx = (A.max_frames + kChunk - 1) / kChunk;
   const int n_items = gx * A.batch;
@@ -848,13 +867,13 @@ __device__ __forceinline__ void bin_cov_sums(const ChainArgs& A, int b, int k, i
 // partials of up to four chunks per round trip through a buffer descriptor covering
 // exactly the utterance's nch chunks, so the loads of absent chunks read +0 without
 // branches and the sums (chunk order kept, + 0 changes nothing) are bitwise those above.
-template <int N, bool SPLIT = true>
+template <int N, bool SPLIT = true, int VF = 4>
 __device__ __forceinline__ void bin_cov_sums_utt(const ChainArgs& A, int b, int k, int nch,
                                                  double (&R)[5]) {
   constexpr int F = N / 2 + 1;
   if (SPLIT && A.a_pieces > 1 &&
       (long long)b * ((A.max_frames + kChunk - 1) / kChunk) + nch > A.a_whole) {
-    bin_cov_sums<N, 4>(A, b, k, nch, R);  // some of its chunks were split (block-uniform)
+    bin_cov_sums<N, VF>(A, b, k, nch, R);  // some of its chunks were split (block-uniform)
     return;
   }
   const rsrc_t rp = make_rsrc(A.part + (long long)b * A.nchunk * 5 * F, (long long)nch * 5 * F);
@@ -874,7 +893,6 @@ __device__ __forceinline__ void bin_cov_sums_utt(const ChainArgs& A, int b, int 
 #pragma unroll
   for (int q = 0; q < 4; ++q) R[q] *= 0.25;
 }
-
 template <int N, bool SPLIT = false>
 __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   constexpr int H = N / 2, F = N / 2 + 1;
@@ -1437,12 +1455,20 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
   // s_whole, then the pieces q = g - s_whole of the utterances [s_whole, batch) (ChainArgs
   // s_pieces, s_steps): utterance s_whole + q / s_pieces, its steps [p s_steps, (p + 1) s_steps),
   // p = q % s_pieces (the host splits only a partial last round or a batch below the CU
-  // count). A whole utterance with a bad device length (host validates) reports NaN, as
-  // finalize does; such an utterance's pieces, and pieces past an utterance's last step, are
-  // skipped (the piece finalize reports the NaN).
+  // count). With the in-kernel piece finalize (s_ipf: the batch has whole rounds, and its
+  // rem * s_pieces piece units fit one round) the pieces come FIRST: unit index g < G is
+  // piece q = g (none for g >= rem * s_pieces), g >= G whole utterance g - G, so every block
+  // runs at most one piece and then its whole utterances, during which the piece's interior
+  // is rescaled once its utterance's last piece has published 1/peak. A whole utterance with
+  // a bad device length (host validates) reports NaN, as finalize does; such an utterance's
+  // pieces, and pieces past an utterance's last step, are skipped (its first piece, or the
+  // piece finalize kernel, reports the NaN).
   const int pieces = PIECES && A.s_pieces > 0 ? A.s_pieces : 0;
   const int s_whole = pieces > 0 ? A.s_whole : A.batch;
-  const int n_units = s_whole + (A.batch - s_whole) * pieces;
+  const bool ipf = PIECES && pieces > 0 && A.s_ipf;
+  const int G = gridDim.x;
+  const int n_pu = (A.batch - s_whole) * pieces;  // piece units
+  const int n_units = ipf ? G + s_whole : s_whole + n_pu;
   struct Unit {
     int g, b, s_lo, s_hi, slot;  // slot: the piece's seam slot, -1 for a whole utterance
   };
@@ -1450,17 +1476,22 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     for (; g < n_units; g += gridDim.x) {
       // lengths read back as block-uniform values: a loop exit decided on a vector load
       // made the next unit's buffer descriptors divergent (a waterfall loop per load)
-      if (g < s_whole) {
-        const int Lg = __builtin_amdgcn_readfirstlane(utt_len(A, g));
-        if (Lg >= N) return Unit{g, g, 0, ((Lg + H - 1) / H + 1 + FB - 1) / FB, -1};
-        if (tid == 0 && A.peak) A.peak[g] = __builtin_nanf("");
+      const bool is_whole = ipf ? g >= G : g < s_whole;
+      if (is_whole) {
+        const int gw = ipf ? g - G : g;
+        const int Lg = __builtin_amdgcn_readfirstlane(utt_len(A, gw));
+        if (Lg >= N) return Unit{g, gw, 0, ((Lg + H - 1) / H + 1 + FB - 1) / FB, -1};
+        if (tid == 0 && A.peak) A.peak[gw] = __builtin_nanf("");
         continue;
       }
       const int pc = pieces > 0 ? pieces : 1;  // (0 only in the whole-rounds instance)
-      const int q = g - s_whole, bq = s_whole + q / pc, lo = (q % pc) * A.s_steps;
+      const int q = ipf ? g : g - s_whole;
+      if (q >= n_pu) continue;
+      const int bq = s_whole + q / pc, lo = (q % pc) * A.s_steps;
       const int Lq = __builtin_amdgcn_readfirstlane(utt_len(A, bq));
       const int ns = ((Lq + H - 1) / H + 1 + FB - 1) / FB;
       if (Lq >= N && lo < ns) return Unit{g, bq, lo, min(ns, lo + A.s_steps), q};
+      if (ipf && Lq < N && lo == 0 && tid == 0 && A.peak) A.peak[bq] = __builtin_nanf("");
     }
     return Unit{n_units, A.batch, 0, 0, -1};
   };
@@ -1488,7 +1519,32 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       });
     }
   };
+  // the utterance's bins solved into the LDS coefficient table (SOLVE)
+  auto solve_coefs = [&](int bb, int TT, auto vf) {
+    constexpr int VF = decltype(vf)::value;
+    float4* ct = reinterpret_cast<float4*>(lds + UttGeo::COEF_OFF);
+    const int nch = (TT + kChunk - 1) / kChunk;
+    for (int k = tid; k < F; k += kUttThreads) {
+      double R[5], w[4];
+      bin_cov_sums_utt<N, PIECES, VF>(A, bb, k, nch, R);
+      const double* d = A.steer + 4 * k;
+      mvdr_weights_d(R, k, N, A, d[0], d[1], d[2], d[3], w, nullptr);
+      cf al, be;
+      coef_from_w(w[0], w[1], w[2], w[3], al, be, nullptr);
+      ct[k] = make_float4(al.x, al.y, be.x, be.y);
+    }
+  };
   Unit cu = unit_at(blockIdx.x);
+  // A piece (the block's first unit) solves before any sample is loaded: its utterance's
+  // chunks may have been split by the analysis tail (up to 8 partial vectors per chunk),
+  // summed 16 vectors per round trip with the registers the samples would hold (with the
+  // samples in flight, 8 per round trip spilled)
+  bool coefs_ready = false;
+  if (PIECES && SOLVE && cu.slot >= 0) {
+    const int Lp = __builtin_amdgcn_readfirstlane(utt_len(A, cu.b));
+    solve_coefs(cu.b, (Lp + H - 1) / H + 1, std::integral_constant<int, 16>{});
+    coefs_ready = true;
+  }
   if (cu.b < A.batch) {
     rsrc_t a0, a1;
     rsrcs(cu.b, a0, a1);
@@ -1503,34 +1559,146 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
   constexpr int RS_U = 4;   // float4 groups per thread per slice (8 slices cover 4 s)
   constexpr int RS_UP = 8;   // the same during a piece's steps (4 slices cover 4 s)
   constexpr int RS_BULK = 32;  // after the loop: a 4-s utterance in one round trip of loads
-  auto rescale_slice = [&](auto uc, int lo, int hi, auto issue_more) {
+  // s_ipf: a piece's own interior waits for its utterance's 1/peak (pstate[rs_lazy].fin, piece
+  // rs_lp): each slice loads it beside the output and stores only once it is published
+  int rs_lazy = -1, rs_lp = 0;
+  uint32_t* redu = reinterpret_cast<uint32_t*>(red);  // red[8 ..]: block-uniform hand-offs
+  auto rescale_slice = [&](auto uc, int lo, int hi, auto issue_more) -> bool {
     constexpr int U = decltype(uc)::value;
     const rsrc_t ro = make_rsrc(rs_out, 4LL * rs_n4);
+    int tq = tid;
+    if constexpr (PIECES) opaque_i(tq);  // offsets recomputed per slice (hoisted, they spilled)
     float4 x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const v4i_t d = __builtin_amdgcn_raw_buffer_load_b128(ro, 16 * (lo + u * kUttThreads + tid), 0,
+      const v4i_t d = __builtin_amdgcn_raw_buffer_load_b128(ro, 16 * (lo + u * kUttThreads + tq), 0,
                                                             kSC1);
       x[u] = make_float4(__int_as_float(d.x), __int_as_float(d.y), __int_as_float(d.z),
                          __int_as_float(d.w));
     }
+    uint32_t fb = 0;
+    if (PIECES && rs_lazy >= 0)
+      fb = __hip_atomic_load(&A.pstate[rs_lazy].fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     issue_more();  // work that overlaps the loads
+    if (PIECES && rs_lazy >= 0) {
+      fb = __builtin_amdgcn_readfirstlane(fb);
+      if (fb == 0u) return false;  // not yet published: this slice again next step
+      rs_scale = __uint_as_float(fb);
+      rs_lazy = -1;
+    }
     float4* o4 = reinterpret_cast<float4*>(rs_out);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = lo + u * kUttThreads + tid;
+      const int i = lo + u * kUttThreads + tq;
       if (i < hi) {
         x[u].x *= rs_scale; x[u].y *= rs_scale; x[u].z *= rs_scale; x[u].w *= rs_scale;
         o4[i] = x[u];
       }
     }
+    return true;
   };
-  // the pending rescale's remaining part, U float4 loads per thread in flight
+  // the pending rescale's remaining part, U float4 loads per thread in flight (a lazy one
+  // resolved first, rs_resolve)
   auto rescale_rest = [&](auto uc) {
     constexpr int U = decltype(uc)::value;
     for (; rs_done < rs_n4; rs_done += U * kUttThreads)
       rescale_slice(uc, rs_done, min(rs_n4, rs_done + U * kUttThreads), [] {});
     rs_out = nullptr;
+  };
+  // A piece's interior still waiting at its block's next utterance end: take 1/peak if it is
+  // published, else hand the piece back to the last arriver (.st bit p) -- unless that one
+  // has passed it already (bit 32 + p), in which case 1/peak is published by now. Called by
+  // every thread after tid 0's redu[12] / redu[10..11] and a barrier (end-of-unit code).
+  auto rs_resolve = [&]() {
+    const uint32_t fb = redu[12];
+    const unsigned long long st = *reinterpret_cast<const unsigned long long*>(redu + 10);
+    if (fb != 0u) {
+      rs_scale = __uint_as_float(fb);
+    } else if ((st >> (32 + rs_lp)) & 1ull) {
+      rs_scale = __uint_as_float(__builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(&A.pstate[rs_lazy].fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    } else {
+      rs_out = nullptr;  // handed back
+    }
+    rs_lazy = -1;
+  };
+  auto rs_resolve_issue = [&]() {  // tid 0, before that barrier
+    const uint32_t fb =
+        __hip_atomic_load(&A.pstate[rs_lazy].fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    redu[12] = fb;
+    if (fb == 0u)
+      *reinterpret_cast<unsigned long long*>(redu + 10) = atomicOr(&A.pstate[rs_lazy].st, 1ull << rs_lp);
+  };
+  // the float4 groups of piece p's interior segments [p seg, (p + 1) seg - 2] (<= T - 2)
+  auto piece_lo4 = [&](int p, int sg) { return p * sg * H / 4; };
+  auto piece_hi4 = [&](int p, int sg, int T) { return min((p + 1) * sg - 1, T - 1) * H / 4; };
+  // s_ipf: the last piece of utterance b to arrive forms its np - 1 seams (pieces' halves
+  // written through to memory, read the same way) x 1 / sum w^2 -- the OLA's arithmetic --,
+  // takes the utterance peak over them and the pieces' interior maxima, writes the seams
+  // scaled and peak[b], publishes 1/peak and rescales the interiors handed back to it.
+  auto piece_finalize = [&](int b, int T, int np, int sg, float* outb) {
+    // thread-derived offsets recomputed here from an opaque tid (hoisted to the kernel start
+    // they were held through the steps and spilled)
+    int t = tid;
+    opaque_i(t);
+    const long long slot0 = (long long)(b - s_whole) * pieces;
+    const float iw = inv_wsum<N>(t);  // H = kUttThreads: thread t owns sample m = t
+    // seam p = tail of piece p - 1 + head of piece p, 8 seams per round trip through
+    // descriptors covering the np slots (absent ones read +0); raw values to the frame
+    // slots (free at a unit's end) for the scaled write
+    const rsrc_t rt = make_rsrc(A.ptails + slot0 * H, (long long)np * H);
+    const rsrc_t rh = make_rsrc(A.pheads + slot0 * H, (long long)np * H);
+    float* stash = reinterpret_cast<float*>(lds) + t;
+    // the pieces' interior maxima (RMW: after every piece's atomicMax), with the seam loads
+    uint32_t pku = 0u;
+    if (t == 0) pku = atomicMax(A.peak_u + b, 0u);
+    float mx = 0.0f;
+    for (int p0 = 1; p0 < np; p0 += 8) {
+      float sv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int p = p0 + u;
+        sv[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rt, 4 * ((p - 1) * H + t), 0, kSC1)) +
+                __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rh, 4 * (p * H + t), 0, kSC1));
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        sv[u] *= iw;
+        mx = fmaxf(mx, fabsf(sv[u]));
+        if (p0 + u < np) stash[(p0 + u - 1) * H] = sv[u];
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    __syncthreads();  // red[] free
+    if (lane == 0) red[wave] = mx;
+    if (t == 0) redu[9] = pku;
+    __syncthreads();
+    float pk = __uint_as_float(redu[9]);
+#pragma unroll
+    for (int w = 0; w < kUttThreads / 64; ++w) pk = fmaxf(pk, red[w]);
+    const float scale = 1.0f / (pk + A.norm_eps);
+    float* ot = outb + t;
+    for (int p = 1; p < np; ++p) ot[(long long)(p * sg - 1) * H] = stash[(p - 1) * H] * scale;
+    if (t == 0) {
+      if (A.peak) A.peak[b] = pk;
+      __hip_atomic_store(&A.pstate[b].fin, __float_as_uint(scale), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // published before the pass
+      uint32_t hi;
+      asm volatile("v_mov_b32 %0, -1" : "=v"(hi));  // materialised here (hoisted, it spilled)
+      *reinterpret_cast<unsigned long long*>(redu + 10) =
+          atomicOr(&A.pstate[b].st, (unsigned long long)hi << 32);
+    }
+    __syncthreads();
+    const unsigned long long hb = *reinterpret_cast<const unsigned long long*>(redu + 10);
+    for (int p = 0; p < np; ++p)
+      if ((hb >> p) & 1ull) {
+        rs_out = outb;
+        rs_scale = scale;
+        rs_done = piece_lo4(p, sg);
+        rs_n4 = piece_hi4(p, sg, T);
+        rescale_rest(std::integral_constant<int, 2 * RS_U>{});
+      }
   };
   // Across a unit's steps only b and its last step are held (more spilled): a piece is
   // recognised by b >= s_whole, its seam slot and unit index follow from b and the frame.
@@ -1554,21 +1722,13 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       }
     }
     // the utterance's apply coefficients into LDS (read per step, so they hold no registers
-    // through the FFTs); the previous unit's readers finished at its last barrier. A piece
-    // reads the solve kernel's (the host launches it for the piece utterances).
+    // through the FFTs); the previous unit's readers finished at its last barrier. Every
+    // piece of an utterance solves its bins too (no solve launch before the kernel).
     {
       float4* ct = reinterpret_cast<float4*>(lds + UttGeo::COEF_OFF);
-      if (SOLVE && (!PIECES || b < s_whole)) {
-        const int nch = (T + kChunk - 1) / kChunk;
-        for (int k = tid; k < F; k += kUttThreads) {
-          double R[5], w[4];
-          bin_cov_sums_utt<N, PIECES>(A, b, k, nch, R);
-          const double* d = A.steer + 4 * k;
-          mvdr_weights_d(R, k, N, A, d[0], d[1], d[2], d[3], w, nullptr);
-          cf al, be;
-          coef_from_w(w[0], w[1], w[2], w[3], al, be, nullptr);
-          ct[k] = make_float4(al.x, al.y, be.x, be.y);
-        }
+      if (SOLVE) {
+        if (!PIECES || !coefs_ready) solve_coefs(b, T, std::integral_constant<int, 4>{});
+        coefs_ready = false;
       } else {
         const float4* coef = reinterpret_cast<const float4*>(A.coef) + (long long)b * F;
         int k0 = tid;
@@ -1734,7 +1894,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         if (j >= 0 && j <= T - 2) {
           const float4 vb = *reinterpret_cast<const float4*>(cframe(s) + m0);
           if (s == 0 && pstart) {  // a piece's first segment is a seam: its half for the
-            *reinterpret_cast<float4*>(A.pheads + pslot * H + m0) = vb;  // piece finalize
+            store_through(A.pheads + pslot * H, H, m0, vb);  // piece finalize
             continue;
           }
           // the previous frame's half read unconditionally (frame 0's when s = 0) and the
@@ -1756,12 +1916,10 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       if (rs_out != nullptr && rs_done < rs_n4) {  // a slice of the previous utterance's rescale
         if (PIECES && b >= s_whole) {  // a piece's few steps: larger slices
           const int lo = rs_done, hi = min(rs_n4, rs_done + RS_UP * kUttThreads);
-          rescale_slice(std::integral_constant<int, RS_UP>{}, lo, hi, ola);
-          rs_done = hi;
+          if (rescale_slice(std::integral_constant<int, RS_UP>{}, lo, hi, ola)) rs_done = hi;
         } else {
           const int lo = rs_done, hi = min(rs_n4, rs_done + RS_U * kUttThreads);
-          rescale_slice(std::integral_constant<int, RS_U>{}, lo, hi, ola);
-          rs_done = hi;
+          if (rescale_slice(std::integral_constant<int, RS_U>{}, lo, hi, ola)) rs_done = hi;
         }
       } else {
         ola();
@@ -1770,7 +1928,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       // a piece's last half-frame (seam half): a whole utterance's last step never has a
       // segment f0 + FB - 1 <= T - 2 (its last frame is T - 1 <= f0 + FB - 1)
       if (PIECES && sgrp == 0 && !more && f0 + FB - 1 <= T - 2)
-        *reinterpret_cast<float4*>(A.ptails + pslot * H + m0) = carry;
+        store_through(A.ptails + pslot * H, H, m0, carry);
       AVZ_STAMP(9);
       lds_barrier();
       AVZ_STAMP(10);
@@ -1780,13 +1938,38 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     for (int o = 32; o > 0; o >>= 1) peak = fmaxf(peak, __shfl_xor(peak, o, 64));
     if (lane == 0) red[wave] = peak;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool whole = !PIECES || b < s_whole;
+    // s_ipf: a piece interior of this block still waiting for its 1/peak (rs_resolve)
+    const bool resolve = PIECES && ipf && whole && rs_lazy >= 0;
+    if (resolve && tid == 0) rs_resolve_issue();
     __syncthreads();
     float pk = red[0];
 #pragma unroll
     for (int w = 1; w < kUttThreads / 64; ++w) pk = fmaxf(pk, red[w]);
-    const bool whole = !PIECES || b < s_whole;
+    if (resolve) rs_resolve();
     if (!whole) {  // a piece: its interior's max (non-negative floats order as uints)
-      if (tid == 0) atomicMax(A.peak_u + b, __float_as_uint(pk));
+      if (ipf) {
+        // arrival: the seam halves were written through (sc1) and drained above, the
+        // atomicMax completes before the count
+        if (tid == 0) {
+          atomicMax(A.peak_u + b, __float_as_uint(pk));
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          redu[9] = atomicAdd(&A.pstate[b].cnt, 1u);
+        }
+        __syncthreads();
+        const int p = (step - 1) / A.s_steps;
+        const int np = min(pieces, ((T + FB - 1) / FB + A.s_steps - 1) / A.s_steps);
+        if (__builtin_amdgcn_readfirstlane(redu[9]) == (uint32_t)(np - 1))
+          piece_finalize(b, T, np, seg, outb);
+        // its own interior: rescaled in slices once 1/peak is published
+        rs_out = outb;
+        rs_lazy = b;
+        rs_lp = p;
+        rs_done = piece_lo4(p, seg);
+        rs_n4 = piece_hi4(p, seg, T);
+      } else if (tid == 0) {
+        atomicMax(A.peak_u + b, __float_as_uint(pk));
+      }
     } else if (tid == 0 && A.peak) {
       A.peak[b] = pk;
     }
@@ -1800,8 +1983,10 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     }
     __syncthreads();  // red[] of the next unit
     AVZ_STAMP(14);
-    // this unit's index: b (whole) or s_whole + the piece's, (step - 1) / s_steps its piece
-    cu = unit_at((whole ? b : s_whole + (b - s_whole) * pieces + (step - 1) / A.s_steps) +
+    // this unit's index (unit_at): from b (whole) or the piece's q, (step - 1) / s_steps its
+    // piece
+    cu = unit_at((whole ? (ipf ? b + G : b)
+                        : (ipf ? 0 : s_whole) + (b - s_whole) * pieces + (step - 1) / A.s_steps) +
                  gridDim.x);
   }
   // the block's last utterance, after the loop where the sample registers are dead: every
@@ -2366,22 +2551,26 @@ static bool solve_fused(const ChainArgs* a) {
 }
 
 // Work split of the N = 1024 per-utterance synthesis (ChainArgs s_whole / s_pieces /
-// s_steps): with R resident blocks (one per CU), whole utterances for the full rounds
+// s_steps / s_ipf): with R resident blocks (one per CU), whole utterances for the full rounds
 // floor(B / R) R, and the partial last round's rem utterances -- or a whole batch below R --
 // in pieces of s_steps steps (16 frames each) spread over the grid, when that is cheaper than
-// one more round of whole utterances. Cost model in steps of the kernel (~9.5 us at two waves
-// per SIMD): a whole round S steps + 2 (the in-block solve and the exposed rescale of its
-// last utterance); pieces ceil(rem pu / R) s_steps + 2 (the pieces' solve and finalize
-// launches, ~10 us each with their kernel boundaries) + 2 rem / R (the finalize's rescale
+// one more round of whole utterances. Every piece solves its utterance's bins in-block. With
+// full rounds (ipf) the pieces run first and finalize in-kernel (the last arriver forms the
+// seams and the peak, each piece rescales its interior during its block's whole utterance);
+// a batch below R keeps the piece-finalize launch. Cost model in steps of the kernel (~9.5
+// us at two waves per SIMD): a whole round S steps + 2 (the in-block solve and the exposed
+// rescale of its last utterance); pieces ceil(rem pu / R) s_steps + 1 (their solve) + 1 + 2
+// rem / R without ipf (the finalize launch, ~10 us with its kernel boundary, and its rescale
 // traffic).
 struct SynthSplit {
   int whole, pieces, steps, grid;
+  bool ipf;
 };
 static SynthSplit synth_split(const ChainArgs* a) {
   constexpr int FB = UttGeo::FB;
   const int R = resident_cus(), B = a->batch;
   const int S = (a->max_frames + FB - 1) / FB;  // steps of the longest utterance
-  const SynthSplit all_whole{B, 0, S, std::min(B, R)};
+  const SynthSplit all_whole{B, 0, S, std::min(B, R), false};
   if (!a->pheads || !a->ptails || B <= 0) return all_whole;
   const int full = B / R, rem = B - full * R;
   if (rem == 0) return all_whole;
@@ -2392,9 +2581,11 @@ static SynthSplit synth_split(const ChainArgs* a) {
   pu = (S + sp - 1) / sp;
   const long long units = (long long)rem * pu;
   const long long rounds = (units + R - 1) / R;
-  const double c_whole = S + 2.0, c_piece = (double)rounds * sp + 2.0 + 2.0 * rem / R;
+  const bool ipf = full > 0 && units <= R && a->pstate != nullptr;
+  const double c_whole = S + 2.0,
+               c_piece = (double)rounds * sp + 1.0 + (ipf ? 0.0 : 1.0 + 2.0 * rem / R);
   if (c_piece >= c_whole) return all_whole;
-  return SynthSplit{full * R, pu, sp, full > 0 ? R : (int)std::min<long long>(units, R)};
+  return SynthSplit{full * R, pu, sp, full > 0 ? R : (int)std::min<long long>(units, R), ipf};
 }
 
 // Synthesis + output normalisation of the chain and of the stage exports: the per-utterance
@@ -2421,15 +2612,8 @@ static int launch_synth_finalize(const ChainArgs* a0, hipStream_t st, const hipE
       c.s_whole = sp.whole;
       c.s_pieces = sp.pieces;
       c.s_steps = sp.steps;
+      c.s_ipf = sp.ipf ? 1 : 0;
       grid = dim3((unsigned)sp.grid);
-      if (sp.pieces > 0 && fused_solve) {  // the pieces' coefficients: the solve kernel's
-        ChainArgs s = c;
-        s.b_lo = sp.whole;
-        const int n = (int)(((long long)(a->batch - sp.whole) * (N / 2 + 1) + kSolveThreads - 1) /
-                            kSolveThreads);
-        auto ks = c.a_pieces > 1 ? avz_solve_kernel<N, true> : avz_solve_kernel<N, false>;
-        hipExtLaunchKernelGGL(ks, dim3(n), dim3(kSolveThreads), 0, st, evt(0), evt(1), 0, s);
-      }
     }
     if constexpr (N == 1024) {
       constexpr int lds = UttGeo::LDS_BYTES;
@@ -2447,7 +2631,7 @@ static int launch_synth_finalize(const ChainArgs* a0, hipStream_t st, const hipE
                                    : lds_ready<avz_synthesis_utt_kernel<UPF, false, false>>(lds));
       if (!ready) return -3;
       hipExtLaunchKernelGGL(kern, grid, dim3(kUttThreads), lds, st, e0, e1, 0, *a);
-      if (c.s_pieces > 0) {
+      if (c.s_pieces > 0 && !c.s_ipf) {
         const int T = a->max_frames;
         const int n4 = (T - 1) * (N / 2) / 4;
         const int gx = (n4 + kFinPieceU * kCThreads - 1) / (kFinPieceU * kCThreads);
@@ -2619,9 +2803,10 @@ extern "C" int avz_chain_kernels(int n_fft, const ChainArgs* a) {
   bool utt = false, fused = false;
   if (n_fft == 1024) chain_kernels_t<1024>(a, utt, fused);
   if (n_fft == 512) chain_kernels_t<512>(a, utt, fused);
-  // the N = 1024 per-utterance kernel's pieces bring a solve (fused plans) and a finalize
-  const bool pieces = utt && n_fft == 1024 && synth_split(a).pieces > 0;
-  return 1 | (fused && !pieces ? 0 : 2) | 4 | (utt && !pieces ? 0 : 8);
+  // the N = 1024 per-utterance kernel's pieces below whole rounds bring a finalize launch
+  const SynthSplit sp = n_fft == 1024 ? synth_split(a) : SynthSplit{0, 0, 0, 0, false};
+  const bool fin = utt && n_fft == 1024 && sp.pieces > 0 && !sp.ipf;
+  return 1 | (fused ? 0 : 2) | 4 | (utt && !fin ? 0 : 8);
 }
 
 extern "C" int avz_launch_chunked(int n_fft, int mask_mode, const ChainArgs* a, void* stream) {
@@ -2704,6 +2889,8 @@ static int launch_synth_t(const ChainArgs* a, hipStream_t st) {
   if (nch > a->nchunk) return -2;
   // no analysis pass in these stages: it is the analysis kernel that resets peak_u
   if (hipMemsetAsync(a->peak_u, 0, sizeof(uint32_t) * a->batch, st) != hipSuccess) return -3;
+  if (a->pstate && hipMemsetAsync(a->pstate, 0, sizeof(PieceState) * a->batch, st) != hipSuccess)
+    return -3;
   if (a->peak && a->normalize != NORM_PEAK &&
       hipMemsetAsync(a->peak, 0, sizeof(float) * a->batch, st) != hipSuccess)
     return -3;

@@ -11,6 +11,12 @@ enum : int { NORM_NONE = 0, NORM_PEAK = 1 };
 enum : int { BF_MVDR = 0, BF_HYBRID_NULL = 1 };
 
 // Everything the analysis / solve / synthesis / finalize chain needs, passed by value.
+struct PieceState {
+  uint32_t cnt, fin;
+  unsigned long long st;
+};
+static_assert(sizeof(PieceState) == 16, "one 16-B store resets it");
+
 struct ChainArgs {
   int batch;
   const int* len;             // [B] samples per utterance (device; kernels clamp to max_len)
@@ -70,6 +76,14 @@ struct ChainArgs {
   float* ptails;
   int pseam_slots;
   int b_lo;                   // solve / piece-finalize launches: first utterance
+  // In-kernel piece finalize (s_ipf = 1; batches with whole rounds): the piece units run
+  // first, the last piece of utterance b to arrive (pstate[b].cnt) forms its seams and peak
+  // and publishes 1/peak in pstate[b].fin (float bits, 0 = not yet); each piece rescales its
+  // own interior during its block's next utterance, or hands it back to that last arriver
+  // (pstate[b].st: bit p = piece p handed back, bit 32 + p = the last arriver has passed
+  // it). Reset with peak_u by the analysis kernel.
+  int s_ipf;
+  PieceState* pstate;
   void* const* events;        // host-only: (start, stop) hipEvent_t pairs of the 4 launches, or null
   int n_events;               // host-only: how many of them to use (8, or 2: analysis only)
 };

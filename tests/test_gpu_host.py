@@ -137,9 +137,10 @@ def test_plan_timing_modes(gpu_device):
     only (NaN for the rest), 0 turns it off (get_timing then reports an argument error).
     With peak normalisation at N = 1024 the per-utterance synthesis kernel folds finalize
     (and, for plain MVDR plans, the solve) in, which then count 0 -- unless, as for this
-    batch of 4 (below the CU count), it splits the utterances into step pieces, which
-    launch a solve and a piece finalize; without peak normalisation (normalize="none") all
-    four kernels run and are timed."""
+    batch of 4 (below the CU count), it splits the utterances into step pieces, which solve
+    their bins in-block and launch a piece finalize; a batch just above the CU count splits
+    its partial round into pieces that finalize in-kernel (no solve, no finalize launch);
+    without peak normalisation (normalize="none") all four kernels run and are timed."""
     import math
 
     import avz
@@ -156,10 +157,21 @@ def test_plan_timing_modes(gpu_device):
         t = plan.timing()
         assert t["calls"] == 3 and t["analysis"] > 0
         others = [t[k] for k in ("solve", "synthesis", "finalize")]
-        if mode == "all":  # B = 4 < #CU: split into pieces, whose solve and finalize run
-            assert others[0] > 0 and others[1] > 0 and others[2] > 0
+        if mode == "all":  # B = 4 < #CU: split into pieces, whose finalize launch runs
+            assert others[0] == 0 and others[1] > 0 and others[2] > 0
         else:
             assert all(math.isnan(v) for v in others)
+    R = torch.cuda.get_device_properties(gpu_device).multi_processor_count
+    mix2, tgt2, itf2 = synth.make_batch(R + 4, n_samples=32000)
+    d2 = [torch.from_numpy(x).to(gpu_device) for x in (mix2, tgt2, itf2)]
+    plan_i = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
+                          max_batch=R + 4, max_samples=32000)
+    plan_i.set_timing(True)
+    for _ in range(2):
+        plan_i.run(d2[0], ref_tgt=d2[1], ref_int=d2[2])
+    t = plan_i.timing()  # B = #CU + 4: the pieces finalize inside the synthesis launch
+    assert t["calls"] == 2 and t["analysis"] > 0 and t["synthesis"] > 0
+    assert t["solve"] == 0 and t["finalize"] == 0
     plan_n = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
                           normalize="none", max_batch=4, max_samples=32000)
     plan_n.set_timing(True)

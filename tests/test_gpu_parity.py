@@ -413,7 +413,15 @@ def test_split_batches_vs_whole_and_oracle(avz, gpu_device, B):
     torch.cuda.synchronize()
     R = torch.cuda.get_device_properties(gpu_device).multi_processor_count
     whole = avz.MVDRPlan(max_batch=R, **kw)
-    pick = sorted({0, B // 2, max(B - 2, 0), B - 1} | ({255, 256} & set(range(B))))
+    # both sides of the split, and up to 8 of the partial round's (piece) utterances
+    tail = list(range(B // R * R, B)) if B > R else []
+    pick = sorted({0, B // 2, max(B - 2, 0), B - 1} | ({255, 256} & set(range(B))) |
+                  set(tail[::max(1, len(tail) // 8)]))
+    # every utterance peaks at 1 (a piece interior left unscaled would not)
+    ok = lens >= 1024
+    pk = out.abs().amax(dim=1).cpu().numpy()[ok]
+    fin = np.isfinite(pk)
+    assert np.all(np.abs(pk[fin] - 1.0) <= 1e-6), np.abs(pk[fin] - 1.0).max()
     mix, tgt, itf = (x.cpu().numpy() for x in (dm, dt, di))
     for b in pick:
         L = int(lens[b])
