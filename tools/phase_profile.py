@@ -41,6 +41,8 @@ ap.add_argument("--mask", default="ibm")
 ap.add_argument("--normalize", default="peak")
 ap.add_argument("--seconds", type=float, default=4.0)
 ap.add_argument("--synth-variant", type=int, default=-1, help="avz_debug_set_synth_variant")
+ap.add_argument("--rows", default="",
+                help="lo:hi[,lo:hi...] block-row groups to report separately (e.g. 0:8,8:256)")
 ap.add_argument("--utt", action="store_true",
                 help="label slots 4-10, 13-15 as the per-utterance synthesis kernel's phases")
 a = ap.parse_args()
@@ -79,9 +81,16 @@ e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / reps
 us = st.double().cpu().numpy() / reps / 100.0  # 100 MHz ticks -> us
-us = us[us.sum(axis=1) > 0]  # persistent grids: only the launched blocks' rows
-tot = us.sum(axis=1)
 print(f"kernel {ms*1e3:.1f} us/launch (stamped build), B={a.batch}, N={a.n_fft}, mask={a.mask}")
-print(f"per-block stamped total: mean {tot.mean():.1f} us, min {tot.min():.1f}, max {tot.max():.1f}")
-for i, n in enumerate(PHASES):
-    print(f"  {n:10s} {us[:, i].mean():8.1f} us  {100*us[:, i].mean()/tot.mean():5.1f} %")
+groups = [tuple(int(v) for v in g.split(":")) for g in a.rows.split(",")] if a.rows else [None]
+full = us
+for g in groups:
+    us = full[g[0]:g[1]] if g else full
+    us = us[us.sum(axis=1) > 0]  # persistent grids: only the launched blocks' rows
+    tot = us.sum(axis=1)
+    if g:
+        print(f"== block rows {g[0]}:{g[1]}")
+    print(f"per-block stamped total: mean {tot.mean():.1f} us, min {tot.min():.1f}, "
+          f"max {tot.max():.1f}")
+    for i, n in enumerate(PHASES):
+        print(f"  {n:10s} {us[:, i].mean():8.1f} us  {100*us[:, i].mean()/tot.mean():5.1f} %")
