@@ -1388,6 +1388,9 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_syn
 // segments, which reads neighbouring waves' frames. Reference semantics as the two-block
 // kernel + avz_finalize_kernel (oracle_debug.py:80-94, scipy istft's OLA and N/2 trim).
 constexpr int kUttThreads = 512;
+#ifndef AVZ_UTT_NL0
+#define AVZ_UTT_NL0 28
+#endif
 struct UttGeo {
   static constexpr int N = 1024, H = 512, F = 513, FB = 16;  // frames per step: 8 waves x 2
   static constexpr int SLOT = KCfg<1024>::GROUP_BYTES;       // one frame (transpose rows of 34)
@@ -1778,14 +1781,25 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       const int sn = ((more ? f0 + FB : nf0) + my) * H - N / 2 + lm.in0;
       // the next step's loads go out after the apply (issued from inside the forward FFT's
       // last stage, after the FFT or after the inverse measured slower)
+      // (the first NL0 of the 32 sample pairs after the apply, the rest between the inverse's
+      // two DFT stages, under its transpose's LDS round trip)
+      constexpr int NL0 = AVZ_UTT_NL0;
       auto next_loads = [&]() {
         if (il) {
-          static_for<0, 32>([&](auto k) {
+          static_for<0, NL0>([&](auto k) {
             v[k].x = bload_nn(q0, sn + 32 * k);
             v[k].y = bload_nn(q1, sn + 32 * k);
           });
         } else {
           first_loads(q0, q1, 0);  // wave 0, last step: the next utterance (or empty)
+        }
+      };
+      auto next_loads_mid = [&]() {
+        if (il) {
+          static_for<NL0, 32>([&](auto k) {
+            v[k].x = bload_nn(q0, sn + 32 * k);
+            v[k].y = bload_nn(q1, sn + 32 * k);
+          });
         }
       };
       window_fft<N>(v, wc0, fft, utt_frame(lds, my), lm);
@@ -1872,7 +1886,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
           const float we = fmaf(wh_s[0], sk, fmaf(-wh_c[0], ck, 0.25f));
           const float wo = fmaf(wh_s[1], sk, fmaf(-wh_c[1], ck, 0.25f));
           Cp[mhs + 16 * k] = make_float2(x.x * we, -x.y * wo);
-        });
+        }, next_loads_mid);
       }
       AVZ_STAMP(7);
       lds_barrier();

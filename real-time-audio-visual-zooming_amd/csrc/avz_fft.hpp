@@ -470,9 +470,15 @@ struct Fft512x2 {
   // block table tw[k1 * 32 + l] = W1024^{l k1} (W512^{j i} = tw[2 i][j], W512^{4 j i} =
   // tw[8 i][j]), formed per transform as init() forms them (same rounding); the N = 1024
   // per-utterance synthesis runs each frame's real inverse at N/2 with it.
+  // mid(): work issued between the two DFT stages (the transpose's LDS round trip).
   template <class Emit>
   __device__ __forceinline__ static void forward_tw1024_emit(cf (&v)[16], cf* scratch, const cf* tw,
                                                              int lane, Emit&& emit) {
+    forward_tw1024_emit(v, scratch, tw, lane, emit, [] {});
+  }
+  template <class Emit, class Mid>
+  __device__ __forceinline__ static void forward_tw1024_emit(cf (&v)[16], cf* scratch, const cf* tw,
+                                                             int lane, Emit&& emit, Mid&& mid) {
     const int jj = lane & 31, kk = lane & 15, hh = (lane >> 4) & 1;
     const float sg = hh ? -1.0f : 1.0f;
     cf p[4], q[4];
@@ -486,6 +492,7 @@ struct Fft512x2 {
       scratch[kc * 34 + jj] = x;
     });
     __builtin_amdgcn_wave_barrier();
+    mid();
     // unpaired reads: the compiler's ds_read2_b64 pairs bank modulo 32 in 16-lane groups,
     // where the rows 34 complex values apart put lanes kk and kk + 8 on the same banks
     // (2-way conflicts); single ds_read_b64 bank modulo 64 in 32-lane groups: conflict-free
