@@ -893,7 +893,9 @@ __device__ __forceinline__ void bin_cov_sums_utt(const ChainArgs& A, int b, int 
 #pragma unroll
   for (int q = 0; q < 4; ++q) R[q] *= 0.25;
 }
-template <int N, bool SPLIT = false>
+// V: split-chunk partial vectors per round trip (32 for the few threads of a small split
+// batch -- B = 1's 17 chunks x 8 pieces were 17 round trips at 8 --, 8 otherwise)
+template <int N, bool SPLIT = false, int V = 8>
 __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   constexpr int H = N / 2, F = N / 2 + 1;
   const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
@@ -904,7 +906,7 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   const int T = (L + H - 1) / H + 1;
   const int nch = (T + kChunk - 1) / kChunk;
   double R[5];
-  bin_cov_sums<N, 8, SPLIT>(A, b, k, nch, R);
+  bin_cov_sums<N, V, SPLIT>(A, b, k, nch, R);
   if (A.cov_only) {  // covariance stage export
 #pragma unroll
     for (int q = 0; q < 5; ++q) A.cov_out[((long long)b * F + k) * 5 + q] = R[q];
@@ -1388,6 +1390,9 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::SYN_BLOCKS_PER_CU) avz_syn
 // segments, which reads neighbouring waves' frames. Reference semantics as the two-block
 // kernel + avz_finalize_kernel (oracle_debug.py:80-94, scipy istft's OLA and N/2 trim).
 constexpr int kUttThreads = 512;
+#ifndef AVZ_PRESOLVE_V
+#define AVZ_PRESOLVE_V 16
+#endif
 #ifndef AVZ_UTT_NL0
 #define AVZ_UTT_NL0 28
 #endif
@@ -1545,7 +1550,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
   bool coefs_ready = false;
   if (PIECES && SOLVE && cu.slot >= 0) {
     const int Lp = __builtin_amdgcn_readfirstlane(utt_len(A, cu.b));
-    solve_coefs(cu.b, (Lp + H - 1) / H + 1, std::integral_constant<int, 16>{});
+    solve_coefs(cu.b, (Lp + H - 1) / H + 1, std::integral_constant<int, AVZ_PRESOLVE_V>{});
     coefs_ready = true;
   }
   if (cu.b < A.batch) {
@@ -2703,6 +2708,13 @@ static int resident_cus() {
   return v;
 }
 
+// A split batch whose solve has few threads (<= 64 blocks): wide round trips over its many
+// partial vectors pay there (B = 257's tail solve at 32 per round trip was slower).
+template <int N>
+static bool few_solve_threads(const ChainArgs* a) {
+  return (long long)a->batch * (N / 2 + 1) <= 64LL * kSolveThreads;
+}
+
 // Tail splitting of the analysis grid (analysis_items): with G resident blocks, the
 // floor(n / G) G items of the full rounds run whole and the partial last round's items in
 // P step-range pieces each (P <= SA, the steps of a chunk; P * tail <= G, the tail slots), so
@@ -2739,7 +2751,8 @@ static int launch_chunked_t(const ChainArgs* a0, hipStream_t st) {
   const bool split = c.a_pieces > 1;  // the SPLIT instances only then
   auto k1 = split ? avz_analysis_kernel<N, MASK, PF == PF_IRM, true>
                   : avz_analysis_kernel<N, MASK, PF == PF_IRM, false>;
-  auto ks = split ? avz_solve_kernel<N, true> : avz_solve_kernel<N, false>;
+  auto ks = split ? (few_solve_threads<N>(a) ? avz_solve_kernel<N, true, 32> : avz_solve_kernel<N, true>)
+                  : avz_solve_kernel<N, false>;
   if (!(split ? lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM, true>>(lds)
               : lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM, false>>(lds)))
     return -3;
@@ -2873,7 +2886,8 @@ static int launch_cov_t(const ChainArgs* a, hipStream_t st) {
   const bool split = c.a_pieces > 1;
   auto ka = split ? avz_analysis_kernel<N, MASK, false, true>
                   : avz_analysis_kernel<N, MASK, false, false>;
-  auto ks = split ? avz_solve_kernel<N, true> : avz_solve_kernel<N, false>;
+  auto ks = split ? (few_solve_threads<N>(a) ? avz_solve_kernel<N, true, 32> : avz_solve_kernel<N, true>)
+                  : avz_solve_kernel<N, false>;
   hipLaunchKernelGGL(ka, dim3((unsigned)grid), dim3(kCThreads), lds, st, c);
   constexpr int F = N / 2 + 1;
   const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
