@@ -217,9 +217,9 @@ int avz_istft(const avz_plan* plan, int batch, int frames, const float* S, long 
  * timed; a kernel folded into another counts 0: with N = 512 or 1024, peak normalisation
  * and the IBM or no post-filter the per-utterance synthesis kernel folds finalize in, and
  * for plain MVDR plans without the item-level fallback or cov / w outputs the solve too --
- * except that a batch whose partial last round (or a batch below the CU count) the
- * N = 1024 kernel splits into step pieces launches a solve for those utterances and a
- * piece finalize, which the solve / finalize slots then time). Not thread-safe. */
+ * except that a batch below the CU count that the N = 1024 kernel splits into step pieces
+ * launches a piece finalize, which the finalize slot then times; the pieces of a partial
+ * last round after whole rounds finalize inside the synthesis kernel). Not thread-safe. */
 int avz_plan_set_timing(avz_plan* plan, int enable);
 /* Time one avz_mvdr_batch call in `period` (>= 1; default 1): the calls in between carry no
  * events, so a sampled timing run costs the other calls nothing. */
