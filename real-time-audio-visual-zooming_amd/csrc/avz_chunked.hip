@@ -1590,7 +1590,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     issue_more();  // work that overlaps the loads
     if (PIECES && rs_lazy >= 0) {
       fb = __builtin_amdgcn_readfirstlane(fb);
-      if (fb == 0u) return false;  // not yet published: this slice again next step
+      if (fb == 0u || A.dbg_ipf == 2) return false;  // not yet published: again next step
       rs_scale = __uint_as_float(fb);
       rs_lazy = -1;
     }
@@ -1630,12 +1630,17 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     }
     rs_lazy = -1;
   };
+  // A hand-back passes the interior (written by this block's plain stores, complete since
+  // the piece's end) to another block on any XCD: released (L2 write-back) before the bit.
+  auto hand_back = [&](int bb, int p) -> unsigned long long {  // tid 0
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    return atomicOr(&A.pstate[bb].st, 1ull << p);
+  };
   auto rs_resolve_issue = [&]() {  // tid 0, before that barrier
     const uint32_t fb =
         __hip_atomic_load(&A.pstate[rs_lazy].fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     redu[12] = fb;
-    if (fb == 0u)
-      *reinterpret_cast<unsigned long long*>(redu + 10) = atomicOr(&A.pstate[rs_lazy].st, 1ull << rs_lp);
+    if (fb == 0u) *reinterpret_cast<unsigned long long*>(redu + 10) = hand_back(rs_lazy, rs_lp);
   };
   // the float4 groups of piece p's interior segments [p seg, (p + 1) seg - 2] (<= T - 2)
   auto piece_lo4 = [&](int p, int sg) { return p * sg * H / 4; };
@@ -1694,8 +1699,10 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // published before the pass
       uint32_t hi;
       asm volatile("v_mov_b32 %0, -1" : "=v"(hi));  // materialised here (hoisted, it spilled)
-      *reinterpret_cast<unsigned long long*>(redu + 10) =
-          atomicOr(&A.pstate[b].st, (unsigned long long)hi << 32);
+      const unsigned long long old = atomicOr(&A.pstate[b].st, (unsigned long long)hi << 32);
+      *reinterpret_cast<unsigned long long*>(redu + 10) = old;
+      // interiors handed back: their owners' writes, released before their bits, acquired
+      if ((uint32_t)old != 0u) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
     const unsigned long long hb = *reinterpret_cast<const unsigned long long*>(redu + 10);
@@ -1978,14 +1985,22 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         __syncthreads();
         const int p = (step - 1) / A.s_steps;
         const int np = min(pieces, ((T + FB - 1) / FB + A.s_steps - 1) / A.s_steps);
-        if (__builtin_amdgcn_readfirstlane(redu[9]) == (uint32_t)(np - 1))
-          piece_finalize(b, T, np, seg, outb);
+        const bool fin_here = __builtin_amdgcn_readfirstlane(redu[9]) == (uint32_t)(np - 1);
+        if (fin_here) piece_finalize(b, T, np, seg, outb);
         // its own interior: rescaled in slices once 1/peak is published
         rs_out = outb;
         rs_lazy = b;
         rs_lp = p;
         rs_done = piece_lo4(p, seg);
         rs_n4 = piece_hi4(p, seg, T);
+        if (A.dbg_ipf == 1 && !fin_here) {  // diagnostic: hand back at once (rs_resolve)
+          if (tid == 0) {
+            redu[12] = 0u;
+            *reinterpret_cast<unsigned long long*>(redu + 10) = hand_back(b, p);
+          }
+          __syncthreads();
+          rs_resolve();
+        }
       } else if (tid == 0) {
         atomicMax(A.peak_u + b, __float_as_uint(pk));
       }
@@ -2540,6 +2555,13 @@ static int resident_cus();
 // per-utterance kernel for N = 1024 time-domain input (no finalize launch), 0 = the
 // two-block chunk kernel + avz_finalize_kernel.
 static std::atomic<int> g_synth_variant{2};
+// In-kernel piece finalize's rare paths forced (tests): ChainArgs::dbg_ipf.
+static std::atomic<int> g_dbg_ipf{0};
+extern "C" int avz_debug_set_ipf_mode(int m) {
+  if (m < 0 || m > 2) return -1;
+  g_dbg_ipf.store(m);
+  return 0;
+}
 extern "C" int avz_debug_set_synth_variant(int v) {
   if (v < 0 || v > 2) return -1;
   g_synth_variant.store(v);
@@ -2632,6 +2654,7 @@ static int launch_synth_finalize(const ChainArgs* a0, hipStream_t st, const hipE
       c.s_pieces = sp.pieces;
       c.s_steps = sp.steps;
       c.s_ipf = sp.ipf ? 1 : 0;
+      c.dbg_ipf = g_dbg_ipf.load(std::memory_order_relaxed);
       grid = dim3((unsigned)sp.grid);
     }
     if constexpr (N == 1024) {

@@ -84,6 +84,9 @@ struct ChainArgs {
   // it). Reset with peak_u by the analysis kernel.
   int s_ipf;
   PieceState* pstate;
+  int dbg_ipf;                // diagnostic (avz_debug_set_ipf_mode): 1 = every piece but the
+                              // last arriver hands itself back at once, 2 = pieces ignore 1/peak
+                              // until their next utterance's end (the protocol's rare paths)
   void* const* events;        // host-only: (start, stop) hipEvent_t pairs of the 4 launches, or null
   int n_events;               // host-only: how many of them to use (8, or 2: analysis only)
 };

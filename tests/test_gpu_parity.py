@@ -385,6 +385,47 @@ def test_multi_round_ragged_batch_equals_single_runs(avz, gpu_device, mask, n_ff
     assert torch.allclose(amax[ok], torch.ones_like(amax[ok]), rtol=1e-6, atol=0)
 
 
+@pytest.mark.parametrize("B", [257, 300])
+def test_piece_finalize_rare_paths_bitwise(avz, gpu_device, B):
+    """The in-kernel piece finalize's rare paths, forced through the diagnostic
+    avz_debug_set_ipf_mode, give the normal path's output bitwise: (1) every piece but its
+    utterance's last arriver hands its interior back at once -- the last arriver rescales the
+    pieces that did so before its pass, the others take 1/peak from the pass bit; (2) pieces
+    ignore the published 1/peak during their block's next utterance and resolve it at its
+    end. The rescale is the same product either way, so outputs and peaks are equal."""
+    from avz import synth
+    from avz._lib import lib
+    S = 64000
+    dm, dt, di = synth.make_batch_device(B, start=77, n_samples=S, n_interferers=2,
+                                         device=gpu_device, rng="philox")
+    lens = np.full(B, S, np.int32)
+    lens[2::5] = np.random.default_rng(B).integers(1024, S + 1, size=len(lens[2::5]))
+    lt = torch.from_numpy(lens).to(gpu_device)
+    plan = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
+                        normalize="peak", max_batch=B, max_samples=S)
+    runs = []
+    try:
+        for mode in (0, 1, 2, 0):
+            assert lib.avz_debug_set_ipf_mode(mode) == 0
+            out, peak = plan.run(dm, lt, max_len=S, ref_tgt=dt, ref_int=di)
+            torch.cuda.synchronize()
+            runs.append((out.clone(), peak.clone()))
+    finally:
+        lib.avz_debug_set_ipf_mode(0)
+    o0, p0 = runs[0]
+    # the valid part of each row (past an utterance's output the row is not written)
+    n_out = torch.tensor([plan.out_len(int(L)) for L in lens], device=gpu_device)
+    valid = torch.arange(o0.shape[1], device=gpu_device)[None, :] < n_out[:, None]
+    for o, p in runs[1:]:
+        same = (o == o0) | (torch.isnan(o) & torch.isnan(o0)) | ~valid
+        assert bool(same.all()), torch.nonzero(~same)[:8].tolist()
+        assert torch.equal(torch.nan_to_num(p, nan=7.0), torch.nan_to_num(p0, nan=7.0))
+    ok = torch.from_numpy(lens >= 1024).to(gpu_device)
+    amax = torch.where(valid, o0.abs(), torch.zeros_like(o0)).amax(dim=1)[ok]
+    fin = torch.isfinite(amax)
+    assert torch.allclose(amax[fin], torch.ones_like(amax[fin]), rtol=1e-6, atol=0)
+
+
 @pytest.mark.parametrize("B", [1, 64, 257, 300])
 def test_split_batches_vs_whole_and_oracle(avz, gpu_device, B):
     """Batches that do not fill whole rounds of the persistent grids (configs[1]'s chain at
@@ -419,7 +460,9 @@ def test_split_batches_vs_whole_and_oracle(avz, gpu_device, B):
                   set(tail[::max(1, len(tail) // 8)]))
     # every utterance peaks at 1 (a piece interior left unscaled would not)
     ok = lens >= 1024
-    pk = out.abs().amax(dim=1).cpu().numpy()[ok]
+    n_out = torch.tensor([plan.out_len(int(L)) for L in lens], device=gpu_device)
+    valid = torch.arange(out.shape[1], device=gpu_device)[None, :] < n_out[:, None]
+    pk = torch.where(valid, out.abs(), torch.zeros_like(out)).amax(dim=1).cpu().numpy()[ok]
     fin = np.isfinite(pk)
     assert np.all(np.abs(pk[fin] - 1.0) <= 1e-6), np.abs(pk[fin] - 1.0).max()
     mix, tgt, itf = (x.cpu().numpy() for x in (dm, dt, di))
