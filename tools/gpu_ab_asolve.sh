@@ -1,5 +1,5 @@
 #!/bin/bash
-# Analysis-side solve: every GPU test on libavz.so (= libavz_I.so), then A/B against
+# Staged partials (or any candidate): every GPU test on libavz.so (= libavz_I.so), then A/B against
 # libavz_A.so on the configurations with >= 2 synthesis rounds and the headline.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
