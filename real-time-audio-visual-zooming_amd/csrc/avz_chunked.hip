@@ -893,20 +893,13 @@ __device__ __forceinline__ void bin_cov_sums_utt(const ChainArgs& A, int b, int 
 #pragma unroll
   for (int q = 0; q < 4; ++q) R[q] *= 0.25;
 }
-// V: split-chunk partial vectors per round trip (32 for the few threads of a small split
-// batch -- B = 1's 17 chunks x 8 pieces were 17 round trips at 8 --, 8 otherwise)
-template <int N, bool SPLIT = false, int V = 8>
-__global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
-  constexpr int H = N / 2, F = N / 2 + 1;
-  const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
-  if (idx >= (long long)(A.batch - A.b_lo) * F) return;
-  const int b = A.b_lo + (int)(idx / F), k = (int)(idx % F);  // b_lo: a piece utterances' solve
-  const int L = utt_len(A, b);
-  if (L < N) return;
-  const int T = (L + H - 1) / H + 1;
-  const int nch = (T + kChunk - 1) / kChunk;
-  double R[5];
-  bin_cov_sums<N, V, SPLIT>(A, b, k, nch, R);
+// The solve of bin k of utterance b from its covariance sums: closed-form MVDR or hybrid
+// hard-null weights with the plan's steering table -> coef[b][k] (+ the cov / w debug
+// outputs, the cov-only stage export, the item-level fallback flag).
+template <int N>
+__device__ __forceinline__ void solve_bin_out(const ChainArgs& A, int b, int k,
+                                              const double (&R)[5]) {
+  constexpr int F = N / 2 + 1;
   if (A.cov_only) {  // covariance stage export
 #pragma unroll
     for (int q = 0; q < 5; ++q) A.cov_out[((long long)b * F + k) * 5 + q] = R[q];
@@ -929,6 +922,77 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
 #pragma unroll
     for (int q = 0; q < 5; ++q) A.cov_out[((long long)b * F + k) * 5 + q] = R[q];
   }
+}
+
+template <int N, bool SPLIT = false>
+__global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
+  constexpr int H = N / 2, F = N / 2 + 1;
+  const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
+  if (idx >= (long long)(A.batch - A.b_lo) * F) return;
+  const int b = A.b_lo + (int)(idx / F), k = (int)(idx % F);  // b_lo: a piece utterances' solve
+  const int L = utt_len(A, b);
+  if (L < N) return;
+  const int T = (L + H - 1) / H + 1;
+  const int nch = (T + kChunk - 1) / kChunk;
+  double R[5];
+  bin_cov_sums<N, 8, SPLIT>(A, b, k, nch, R);
+  solve_bin_out<N>(A, b, k, R);
+}
+
+// The solve of a small split batch (few bins, many partial vectors each: B = 1's 8.23-s
+// triple at 512/256 has 17 chunks x 8 pieces): kSolveLanes lanes per bin, each summing a
+// contiguous run of the bin's partial vectors (the whole chunks', then the split chunks'
+// pieces, bin_cov_sums' order) in fp64, combined by a fixed xor tree -- deterministic, and
+// the association differs from the sequential sum only by fp64 rounding. One round trip of
+// 20 vectors per lane (160 per bin) where the sequential thread took 17 of 8.
+constexpr int kSolveLanes = 8;
+template <int N>
+__global__ void __launch_bounds__(kSolveThreads) avz_solve_lanes_kernel(ChainArgs A) {
+  constexpr int H = N / 2, F = N / 2 + 1, V = 20;
+  const int sub = threadIdx.x % kSolveLanes;
+  const long long idx = (long long)blockIdx.x * (kSolveThreads / kSolveLanes) +
+                        threadIdx.x / kSolveLanes;
+  // no early exit: a bin's lanes all take part in the tree (a group is 8 aligned lanes)
+  const bool live = idx < (long long)(A.batch - A.b_lo) * F;
+  const int b = A.b_lo + (live ? (int)(idx / F) : 0), k = live ? (int)(idx % F) : 0;
+  const int L = utt_len(A, b);
+  const bool ok = live && L >= N;
+  const int T = (max(L, N) + H - 1) / H + 1;
+  const int nch = (T + kChunk - 1) / kChunk;
+  const long long it0 = (long long)b * ((A.max_frames + kChunk - 1) / kChunk);
+  const int cw = A.a_pieces > 1 ? (int)max(0LL, min((long long)nch, A.a_whole - it0)) : nch;
+  const int nvec = cw + (nch - cw) * (A.a_pieces > 1 ? A.a_pieces : 0);
+  const rsrc_t rp = make_rsrc(A.part + (long long)b * A.nchunk * 5 * F, (long long)cw * 5 * F);
+  const rsrc_t rt = cw < nch ? make_rsrc(A.tpart + (it0 + cw - A.a_whole) * A.a_pieces * 5 * F,
+                                         (long long)(nvec - cw) * 5 * F)
+                             : make_rsrc(nullptr, 0);
+  const int per = (nvec + kSolveLanes - 1) / kSolveLanes;
+  const int v_lo = sub * per, v_hi = min(nvec, v_lo + per);
+  double R[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) R[q] = 0.0;
+  for (int v0 = v_lo; v0 < v_hi; v0 += V) {
+    float pv[V][5];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int v = v0 + i;  // past v_hi: read, not summed
+#pragma unroll
+      for (int q = 0; q < 5; ++q)
+        pv[i][q] = v < cw ? bload(rp, (v * 5 + q) * F + k) : bload(rt, ((v - cw) * 5 + q) * F + k);
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i)
+      if (v0 + i < v_hi)
+#pragma unroll
+        for (int q = 0; q < 5; ++q) R[q] += (double)pv[i][q];
+  }
+#pragma unroll
+  for (int o = 1; o < kSolveLanes; o <<= 1)
+#pragma unroll
+    for (int q = 0; q < 5; ++q) R[q] += __shfl_xor(R[q], o, kSolveLanes);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) R[q] *= 0.25;
+  if (ok && sub == 0) solve_bin_out<N>(A, b, k, R);
 }
 
 // batch_mvdr's item-level fallback (AVZ_FALLBACK_BATCH): the items whose solve met a
@@ -2629,6 +2693,18 @@ static SynthSplit synth_split(const ChainArgs* a) {
   return SynthSplit{full * R, pu, sp, full > 0 ? R : (int)std::min<long long>(units, R), ipf};
 }
 
+// A split batch whose solve has few threads (<= 64 blocks of one bin per thread): its many
+// partial vectors per bin go to kSolveLanes lanes per bin (avz_solve_lanes_kernel).
+template <int N>
+static bool few_solve_threads(const ChainArgs* a) {
+  return (long long)a->batch * (N / 2 + 1) <= 64LL * kSolveThreads;
+}
+template <int N>
+static int solve_blocks(const ChainArgs* a, bool lanes) {
+  const long long per = lanes ? kSolveThreads / kSolveLanes : kSolveThreads;
+  return (int)(((long long)a->batch * (N / 2 + 1) + per - 1) / per);
+}
+
 // Synthesis + output normalisation of the chain and of the stage exports: the per-utterance
 // kernel (time-domain input, peak normalisation; finalize events record an empty span unless
 // the N = 1024 split has pieces, whose solve and finalize launches the solve and finalize
@@ -2731,13 +2807,6 @@ static int resident_cus() {
   return v;
 }
 
-// A split batch whose solve has few threads (<= 64 blocks): wide round trips over its many
-// partial vectors pay there (B = 257's tail solve at 32 per round trip was slower).
-template <int N>
-static bool few_solve_threads(const ChainArgs* a) {
-  return (long long)a->batch * (N / 2 + 1) <= 64LL * kSolveThreads;
-}
-
 // Tail splitting of the analysis grid (analysis_items): with G resident blocks, the
 // floor(n / G) G items of the full rounds run whole and the partial last round's items in
 // P step-range pieces each (P <= SA, the steps of a chunk; P * tail <= G, the tail slots), so
@@ -2774,13 +2843,13 @@ static int launch_chunked_t(const ChainArgs* a0, hipStream_t st) {
   const bool split = c.a_pieces > 1;  // the SPLIT instances only then
   auto k1 = split ? avz_analysis_kernel<N, MASK, PF == PF_IRM, true>
                   : avz_analysis_kernel<N, MASK, PF == PF_IRM, false>;
-  auto ks = split ? (few_solve_threads<N>(a) ? avz_solve_kernel<N, true, 32> : avz_solve_kernel<N, true>)
-                  : avz_solve_kernel<N, false>;
+  const bool lanes = split && few_solve_threads<N>(a);
+  auto ks = lanes ? avz_solve_lanes_kernel<N>
+                  : (split ? avz_solve_kernel<N, true> : avz_solve_kernel<N, false>);
   if (!(split ? lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM, true>>(lds)
               : lds_ready<avz_analysis_kernel<N, MASK, PF == PF_IRM, false>>(lds)))
     return -3;
-  constexpr int F = N / 2 + 1;
-  const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
+  const int nsolve = solve_blocks<N>(a, lanes), nfix = solve_blocks<N>(a, false);
   // diagnostic timing: kernel i's (start, stop) events ride on its own dispatch packet
   // (hipExtLaunchKernel), so timing adds no marker packets between the launches
   hipEvent_t const* ev = reinterpret_cast<hipEvent_t const*>(a->events);
@@ -2793,7 +2862,7 @@ static int launch_chunked_t(const ChainArgs* a0, hipStream_t st) {
   if (fused) {
   } else if (item_fallback) {
     hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), nullptr, 0, *a);
-    hipExtLaunchKernelGGL(avz_solve_fixup_kernel<N>, dim3(nsolve), dim3(kSolveThreads), 0, st,
+    hipExtLaunchKernelGGL(avz_solve_fixup_kernel<N>, dim3(nfix), dim3(kSolveThreads), 0, st,
                           nullptr, evt(3), 0, *a);
   } else {
     hipExtLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, evt(2), evt(3), 0, *a);
@@ -2909,12 +2978,11 @@ static int launch_cov_t(const ChainArgs* a, hipStream_t st) {
   const bool split = c.a_pieces > 1;
   auto ka = split ? avz_analysis_kernel<N, MASK, false, true>
                   : avz_analysis_kernel<N, MASK, false, false>;
-  auto ks = split ? (few_solve_threads<N>(a) ? avz_solve_kernel<N, true, 32> : avz_solve_kernel<N, true>)
-                  : avz_solve_kernel<N, false>;
+  const bool lanes = split && few_solve_threads<N>(a);
+  auto ks = lanes ? avz_solve_lanes_kernel<N>
+                  : (split ? avz_solve_kernel<N, true> : avz_solve_kernel<N, false>);
   hipLaunchKernelGGL(ka, dim3((unsigned)grid), dim3(kCThreads), lds, st, c);
-  constexpr int F = N / 2 + 1;
-  const int nsolve = (int)(((long long)a->batch * F + kSolveThreads - 1) / kSolveThreads);
-  hipLaunchKernelGGL(ks, dim3(nsolve), dim3(kSolveThreads), 0, st, c);
+  hipLaunchKernelGGL(ks, dim3(solve_blocks<N>(a, lanes)), dim3(kSolveThreads), 0, st, c);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
