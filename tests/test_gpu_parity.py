@@ -385,6 +385,30 @@ def test_multi_round_ragged_batch_equals_single_runs(avz, gpu_device, mask, n_ff
     assert torch.allclose(amax[ok], torch.ones_like(amax[ok]), rtol=1e-6, atol=0)
 
 
+@pytest.mark.parametrize("B", [1, 257])
+def test_split_batch_unfused_solve_bitwise(avz, gpu_device, B):
+    """A split batch with the covariance / weight debug outputs takes the solve kernel and
+    the per-utterance kernel's copying instance (pieces included: B = 1 below the CU count,
+    B = 257 through the in-kernel piece finalize); its outputs and peaks equal the fused
+    in-block solve's bitwise, and the debug covariances are finite for every valid bin."""
+    from avz import synth
+    S = 64000
+    dm, dt, di = synth.make_batch_device(B, start=901, n_samples=S, n_interferers=2,
+                                         device=gpu_device, rng="philox")
+    plan = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
+                        normalize="peak", max_batch=B, max_samples=S)
+    out, peak = plan.run(dm, ref_tgt=dt, ref_int=di)
+    out, peak = out.clone(), peak.clone()
+    cov = torch.empty((B, 513, 5), dtype=torch.float64, device=gpu_device)
+    w = torch.empty((B, 513, 4), dtype=torch.float32, device=gpu_device)
+    out_d, peak_d = plan.run(dm, ref_tgt=dt, ref_int=di, cov_out=cov, w_out=w)
+    torch.cuda.synchronize()
+    n = plan.out_len(S)
+    assert torch.equal(out[:, :n], out_d[:, :n])
+    assert torch.equal(peak, peak_d)
+    assert bool(torch.isfinite(cov).all())
+
+
 @pytest.mark.parametrize("B", [257, 300])
 def test_piece_finalize_rare_paths_bitwise(avz, gpu_device, B):
     """The in-kernel piece finalize's rare paths, forced through the diagnostic
