@@ -929,7 +929,7 @@ __global__ void __launch_bounds__(kSolveThreads) avz_solve_kernel(ChainArgs A) {
   constexpr int H = N / 2, F = N / 2 + 1;
   const long long idx = (long long)blockIdx.x * kSolveThreads + threadIdx.x;
   if (idx >= (long long)(A.batch - A.b_lo) * F) return;
-  const int b = A.b_lo + (int)(idx / F), k = (int)(idx % F);  // b_lo: a piece utterances' solve
+  const int b = A.b_lo + (int)(idx / F), k = (int)(idx % F);  // b_lo: first utterance solved
   const int L = utt_len(A, b);
   if (L < N) return;
   const int T = (L + H - 1) / H + 1;

@@ -75,7 +75,7 @@ struct ChainArgs {
   float* pheads;
   float* ptails;
   int pseam_slots;
-  int b_lo;                   // solve / piece-finalize launches: first utterance
+  int b_lo;                   // solve launches: first utterance solved (0 in the chain)
   // In-kernel piece finalize (s_ipf = 1; batches with whole rounds): the piece units run
   // first, the last piece of utterance b to arrive (pstate[b].cnt) forms its seams and peak
   // and publishes 1/peak in pstate[b].fin (float bits, 0 = not yet); each piece rescales its
