@@ -1457,8 +1457,11 @@ constexpr int kUttThreads = 512;
 #ifndef AVZ_PRESOLVE_V
 #define AVZ_PRESOLVE_V 16
 #endif
+#ifndef AVZ_UTT_SHARE
+#define AVZ_UTT_SHARE 1
+#endif
 #ifndef AVZ_UTT_NL0
-#define AVZ_UTT_NL0 28
+#define AVZ_UTT_NL0 32
 #endif
 struct UttGeo {
   static constexpr int N = 1024, H = 512, F = 513, FB = 16;  // frames per step: 8 waves x 2
@@ -1490,11 +1493,27 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // 0..7
   const int lane = tid & 63;
+  // SHARE: a wave's two frames (2 wave, 2 wave + 1) overlap by N/2 and are loaded as in the
+  // analysis kernel (pair_loads: 24 sample pairs per lane instead of 32, lane group 1's frame
+  // rotated by N/2): its window halves swapped (ac, as negated) and its spectrum's (-1)^k
+  // undone by (-1)^k1 on the stage-1 twiddles (the odd j factors twa[j - 1] of k1 = 8 m + j)
+  constexpr bool SHARE = AVZ_UTT_SHARE;
   Fft1024x2 fft;
   fft.init(lane);
   LaneMap<N> lm;
   lm.init(lane);
-  const WinCoef<N> wc0 = [&] { WinCoef<N> w; w.init(lm); return w; }();
+  if (SHARE && lm.grp) {
+    static_for<0, 4>([&](auto i) { fft.twa[2 * i] = cf{-fft.twa[2 * i].x, -fft.twa[2 * i].y}; });
+  }
+  const WinCoef<N> wc0 = [&] {
+    WinCoef<N> w;
+    w.init(lm);
+    if (SHARE && lm.grp) {
+      w.ac = -w.ac;
+      w.as = -w.as;
+    }
+    return w;
+  }();
   const int my = 2 * wave + lm.grp;  // frame of the step = slot
   // apply bins: m_j = lane + 64 j (j < 4) pairs bin kA = m with kB = N/2 - m; bin N/4 (its
   // own partner) on lanes 0 (frame 2 wave) and 1 (frame 2 wave + 1)
@@ -1516,9 +1535,7 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     wh_s[e] = (float)(0.25 * sn);
   }
   // overlap-add role: 4 consecutive samples m0.. of segments sgrp + 4 si
-  float inv[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(4 * (tid & 127) + i);
+  float inv[4];  // (filled after a first piece's pre-solve: live across it, they spilled)
   __syncthreads();  // twiddle table
   AVZ_STAMP_DECL();
   AVZ_STAMP_INIT();
@@ -1578,6 +1595,14 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
   // a unit's first step (frames f0 ..): at f0 = 0 wave 0's first frame starts N/2 before
   // sample 0 (range-checked offsets); every other frame starts at sample >= 0
   auto first_loads = [&](rsrc_t a0, rsrc_t a1, int f0) {
+    if constexpr (SHARE) {
+      const int sp = (f0 + 2 * wave) * H - N / 2 + lm.in0;
+      if (wave >= 1 || f0 > 0)
+        pair_loads<true>(v, a0, a1, sp, lm.grp);
+      else
+        pair_loads<false>(v, a0, a1, sp, lm.grp);
+      return;
+    }
     const int s0 = (f0 + my) * H - N / 2 + lm.in0;
     if (wave >= 1 || f0 > 0) {
       static_for<0, 32>([&](auto r) {
@@ -1617,6 +1642,8 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     solve_coefs(cu.b, (Lp + H - 1) / H + 1, std::integral_constant<int, AVZ_PRESOLVE_V>{});
     coefs_ready = true;
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) inv[i] = inv_wsum<N>(4 * (tid & 127) + i);
   if (cu.b < A.batch) {
     rsrc_t a0, a1;
     rsrcs(cu.b, a0, a1);
@@ -1854,30 +1881,39 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
         q0 = make_rsrc(qm, ql);
         q1 = make_rsrc(qm + A.ch_stride, ql);
       }
-      const int sn = ((more ? f0 + FB : nf0) + my) * H - N / 2 + lm.in0;
+      const int sn = ((more ? f0 + FB : nf0) + (SHARE ? 2 * wave : my)) * H - N / 2 + lm.in0;
       // the next step's loads go out after the apply (issued from inside the forward FFT's
       // last stage, after the FFT or after the inverse measured slower)
-      // (the first NL0 of the 32 sample pairs after the apply, the rest between the inverse's
-      // two DFT stages, under its transpose's LDS round trip)
+      // (registers k < NL0 after the apply, the rest between the inverse's two DFT stages,
+      // under its transpose's LDS round trip: with 32 loads per lane 28 + 4 measured best
+      // (profiles/r05/ab_next_loads_split.txt), with the 24 of SHARE all after the apply,
+      // profiles/r05/ab_share_loads.txt)
       constexpr int NL0 = AVZ_UTT_NL0;
-      auto next_loads = [&]() {
-        if (il) {
-          static_for<0, NL0>([&](auto k) {
-            v[k].x = bload_nn(q0, sn + 32 * k);
-            v[k].y = bload_nn(q1, sn + 32 * k);
-          });
-        } else {
-          first_loads(q0, q1, 0);  // wave 0, last step: the next utterance (or empty)
+      auto load_k = [&](auto kc) {  // register k's next sample pair (SHARE: as pair_loads)
+        constexpr int k = decltype(kc)::value;
+        if constexpr (!SHARE) {
+          v[k].x = bload_nn(q0, sn + 32 * k);
+          v[k].y = bload_nn(q1, sn + 32 * k);
+        } else if constexpr (k < 16) {
+          const int e = sn + 1024 * lm.grp + 32 * k;
+          v[k].x = bload_nn(q0, e);
+          v[k].y = bload_nn(q1, e);
+        } else if constexpr ((k - 16) % 2 == 0) {
+          const int e = sn + 512 + 32 * (k - 16) + 32 * lm.grp;
+          v[k].x = bload_nn(q0, e);
+          v[k].y = bload_nn(q1, e);
         }
+      };
+      auto next_loads = [&]() {
+        if (il)
+          static_for<0, NL0>(load_k);
+        else
+          first_loads(q0, q1, 0);  // wave 0, last step: the next utterance (or empty)
       };
       auto next_loads_mid = [&]() {
-        if (il) {
-          static_for<NL0, 32>([&](auto k) {
-            v[k].x = bload_nn(q0, sn + 32 * k);
-            v[k].y = bload_nn(q1, sn + 32 * k);
-          });
-        }
+        if (il) static_for<NL0, 32>(load_k);
       };
+      if constexpr (SHARE) pair_finish(v);
       window_fft<N>(v, wc0, fft, utt_frame(lds, my), lm);
       AVZ_STAMP(4);
       __builtin_amdgcn_wave_barrier();
