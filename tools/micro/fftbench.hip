@@ -1,6 +1,10 @@
 // FFT-phase throughput microbenchmark: each block repeats {FFT from registers ->
 // LDS transpose -> natural-order spectrum store -> block barrier} ITERS times.
 // Reports nothing itself; time it from Python (tools/micro/fftbench.py).
+// Builds against the FFT header as it was before commit 4c3751f, which removed the Fft1024
+// (x1) shape and the register-twiddle entry points some variants use (round-2/3 records in
+// DESIGN.md): `git show 4c3751f^:real-time-audio-visual-zooming_amd/csrc/avz_fft.hpp`.
+// The round-5 packed-fp32 comparison is the standalone tools/micro/pkbench.hip.
 #include <hip/hip_runtime.h>
 // the variants below size their LDS for the stride-33 transpose (8448-B groups)
 #define AVZ_TSTRIDE 33
