@@ -105,6 +105,9 @@ def parse():
                     help="N > 1 rehearsal on one GPU: all ranks on cuda:0, gloo collectives")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-kernel HIP events (roofline from the step events)")
+    ap.add_argument("--ibm-kappa", type=float, default=0.0,
+                    help="diagnostic: the IBM plans' certificate constant (avz_config.ibm_kappa; "
+                         "0 = the library default, < 0 = fp32 decisions only)")
     ap.add_argument("--no-settle", action="store_true",
                     help="skip the clock-settling steps before the warmup (cold-GPU timing)")
     a = ap.parse_args()
@@ -238,7 +241,8 @@ def setup_chain(spec, dev, batches):
     norm = "peak" if spec["normalize"] == "peak" else "none"
     if spec["workload"] == "ibm":
         plan = avz.MVDRPlan(n_fft=n_fft, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
-                            normalize=norm, max_batch=B, max_samples=S)
+                            normalize=norm, max_batch=B, max_samples=S,
+                            ibm_kappa=spec.get("ibm_kappa", 0.0))
         streams = 4
     else:
         plan = avz.MVDRPlan(n_fft=n_fft, sigma=1e-7, mic_d=0.01, mask="ipd", postfilter="none",
@@ -514,10 +518,10 @@ def configs0_latency(dev, n_calls=50):
         kt = plan.timing()
         plan.set_timing(False)
         # the round-3 synthesis form for comparison: chunk grid + solve + finalize launches
-        # (avz_debug_set_synth_variant(0); the analysis kernel as above)
-        from avz._lib import lib as _lib
+        # (the plan's diagnostics, synth_variant 0; the analysis kernel as above)
         alt = None
-        if hasattr(_lib, "avz_debug_set_synth_variant") and _lib.avz_debug_set_synth_variant(0) == 0:
+        if True:
+            plan.set_diagnostics(synth_variant=0)
             try:
                 for _ in range(10):
                     call()
@@ -530,7 +534,7 @@ def configs0_latency(dev, n_calls=50):
                     lat0.append(1e3 * (time.perf_counter() - t0))
                 alt = float(np.median(lat0))
             finally:
-                _lib.avz_debug_set_synth_variant(2)
+                plan.set_diagnostics(synth_variant=2)
         call()
         torch.cuda.synchronize()
         n_out = plan.out_len(S)
@@ -691,7 +695,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     spec = dict(workload=args.workload, B=B, k=args.interferers, n_fft=N_FFT,
-                normalize=args.normalize)
+                normalize=args.normalize, ibm_kappa=args.ibm_kappa)
     # this rank's shard(s) of utterances, generated in HBM: batch 0 = utterances rank * B ..
     # rank * B + B - 1 (the one the SIR metrics score), batch 1 = the next world * B
     g0 = time.perf_counter()

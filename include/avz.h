@@ -98,7 +98,17 @@ typedef struct avz_config {
   double cond_max;   /* AVZ_BF_HYBRID_NULL: delay-and-sum above this 2-norm condition
                         number of [v_tgt, v_int] (10, inference.py:80)               */
   int singular_fallback; /* AVZ_FALLBACK_*                                            */
+  double ibm_kappa;  /* AVZ_MASK_IBM, reference-exact decisions (oracle_debug.py:42-53):
+                        every (bin, frame) decision of the fp32 reference transform must
+                        clear an error bound of ibm_kappa * 2^-24 * ||windowed frame||, or
+                        the frame's decision is recomputed from fp64 reference spectra
+                        rounded to complex64 with numpy's |.|.
+                        0 = AVZ_IBM_KAPPA; < 0 = no certificate (fp32 decisions only). */
 } avz_config;
+/* 16: the bound 3.9 kappa eps ||z|| max|Z| covers the largest fp32-transform error seen in
+ * 1.5 M decisions of the configs[1] generator (49 eps ||z|| max|Z|, tools/dbg/kappa_sweep.py
+ * and DESIGN.md section 2) by 1.27x; each doubling of kappa adds ~1 % of the frames. */
+#define AVZ_IBM_KAPPA 16.0
 
 typedef struct avz_plan avz_plan;
 
@@ -225,6 +235,23 @@ int avz_plan_set_timing(avz_plan* plan, int enable);
  * events, so a sampled timing run costs the other calls nothing. */
 int avz_plan_set_timing_period(avz_plan* plan, int period);
 int avz_plan_get_timing(avz_plan* plan, double* ms_avg /*[4]*/, int* calls);
+/* Diagnostics of the reference-exact IBM path (avz_config.ibm_kappa): every later call on
+ * this plan adds to counts[0] the frames decided on the exact path and to counts[1] the
+ * (bin, frame) decisions taken there (device array of two unsigned long long, zeroed by the
+ * caller; NULL = off). Not thread-safe with calls on the plan. */
+int avz_plan_set_ibm_stats(avz_plan* plan, unsigned long long* counts);
+/* Diagnostics: kernel-path A/B of this plan's later calls (tests and tools only; the
+ * results are the same up to the fp32 association of the partial sums):
+ *  synth_variant 2 (default) = the per-utterance synthesis kernel solving its own bins,
+ *  1 = the same after the solve kernel, 0 = the two-block chunk grid + finalize kernel;
+ *  ipf_mode 0 (default) = the in-kernel piece finalize as shipped, 1 = every piece but its
+ *  utterance's last arriver hands its interior back at once, 2 = pieces ignore the published
+ *  1/peak until their next utterance's end (the protocol's rare paths, forced).
+ * Not thread-safe with calls on the plan. */
+int avz_plan_set_diagnostics(avz_plan* plan, int synth_variant, int ipf_mode);
+/* The reference's fp32 analysis window, np.float32(scipy.signal.get_window('hann', n)), as the
+ * exact IBM path uses it (n = 512 or 1024; host memory; for tests). */
+int avz_ibm_window(int n, float* out);
 
 /* Stage API: STFT of [batch][channels][x_stride] real signals into complex64
  * Y[b][c][k][t] (interleaved re/im floats) with element strides; replaces the

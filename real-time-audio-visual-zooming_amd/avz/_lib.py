@@ -7,7 +7,6 @@ from __future__ import annotations
 
 import ctypes as ct
 import os
-import warnings
 
 # PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7). Loading torch
 # first makes libavz.so's NEEDED libamdhip64.so.7 resolve to that same runtime, so
@@ -41,7 +40,8 @@ EXPORTED = [
     "avz_last_hip_error", "avz_version", "avz_mvdr_workspace_bytes",
     "avz_mvdr_covariance", "avz_solve_covariance", "avz_apply_istft", "avz_beamform_spectral",
     "avz_istft", "avz_scene_generate_workspace_bytes", "avz_scene_generate",
-    "avz_projection_metrics_scaled",
+    "avz_projection_metrics_scaled", "avz_plan_set_ibm_stats", "avz_plan_set_diagnostics",
+    "avz_ibm_window",
 ]
 
 
@@ -55,7 +55,7 @@ class AvzConfig(ct.Structure):
         ("normalize", ct.c_int), ("norm_eps", ct.c_double),
         ("max_batch", ct.c_int), ("max_samples", ct.c_int),
         ("beamformer", ct.c_int), ("bypass_hz", ct.c_double), ("cond_max", ct.c_double),
-        ("singular_fallback", ct.c_int),
+        ("singular_fallback", ct.c_int), ("ibm_kappa", ct.c_double),
     ]
 
 
@@ -89,7 +89,7 @@ class AvzError(RuntimeError):
     pass
 
 
-ABI_VERSION = 2
+ABI_VERSION = 3  # INTEGRATION.md section 4 (3: avz_config.ibm_kappa)
 
 
 def hip_runtimes_mapped() -> list:
@@ -136,6 +136,9 @@ def _load():
     lib.avz_plan_set_timing.argtypes = [P, I]
     lib.avz_plan_set_timing_period.argtypes = [P, I]
     lib.avz_plan_get_timing.argtypes = [P, ct.POINTER(ct.c_double), ct.POINTER(I)]
+    lib.avz_plan_set_ibm_stats.argtypes = [P, P]
+    lib.avz_plan_set_diagnostics.argtypes = [P, I, I]
+    lib.avz_ibm_window.argtypes = [I, ct.POINTER(ct.c_float)]
     lib.avz_chunk_split.argtypes = [I, I, I, P, P, P, P, LL, LL, P, LL, LL, P]
     lib.avz_chunk_merge.argtypes = [I, I, I, I, P, P, P, LL, P, LL, P, I, ct.c_double, P]
     lib.avz_mask_features.argtypes = [P, I, I, P, I, P, LL, LL, P, LL, LL, LL, LL, P]
@@ -158,24 +161,12 @@ def _load():
                  "avz_plan_set_timing", "avz_plan_get_timing", "avz_mask_features",
                  "avz_plan_set_timing_period",
                  "avz_srp_scan", "avz_projection_metrics", "avz_scene_mix",
-                 "avz_scene_generate", "avz_projection_metrics_scaled", "avz_version"):
+                 "avz_scene_generate", "avz_projection_metrics_scaled", "avz_version",
+                 "avz_plan_set_ibm_stats", "avz_plan_set_diagnostics", "avz_ibm_window"):
         getattr(lib, name).restype = ct.c_int
-    if lib.avz_version() != ABI_VERSION:  # the struct layouts above are version 2's
+    if lib.avz_version() != ABI_VERSION:  # the struct layouts above are version 3's
         raise ImportError(f"libavz ABI version {lib.avz_version()} != {ABI_VERSION} "
                           "(AvzBatchArgs / AvzSpectralArgs layouts); rebuild")
-    # diagnostic A/B of the synthesis paths (tools/ab_synth.py, bench.py runs): 2 the
-    # per-utterance kernel solving its own bins (default), 1 the same after the solve
-    # kernel, 0 the chunk grid + finalize
-    v = os.environ.get("AVZ_SYNTH_VARIANT")  # diagnostic A/B only (tools/gpu_bench_ab.sh)
-    if v and hasattr(lib, "avz_debug_set_synth_variant"):
-        try:
-            ok = lib.avz_debug_set_synth_variant(int(v)) == 0
-        except ValueError:
-            ok = False
-        if not ok:
-            warnings.warn(f"AVZ_SYNTH_VARIANT={v!r} ignored (expected 0, 1 or 2)")
-        else:
-            warnings.warn(f"AVZ_SYNTH_VARIANT={v}: synthesis path overridden for this process")
     return lib
 
 

@@ -57,6 +57,9 @@ class PlanConfig:
     bypass_hz: float = 200.0
     cond_max: float = 10.0
     singular_fallback: str = "mic0"
+    # AVZ_MASK_IBM: certificate constant of the reference-exact decisions (include/avz.h
+    # avz_config.ibm_kappa): 0 = the library default, < 0 = fp32 decisions only
+    ibm_kappa: float = 0.0
     extra: dict = field(default_factory=dict)
 
 
@@ -91,6 +94,7 @@ class MVDRPlan:
         c.beamformer = BEAMFORMERS[cfg.beamformer]
         c.bypass_hz, c.cond_max = cfg.bypass_hz, cfg.cond_max
         c.singular_fallback = FALLBACKS[cfg.singular_fallback]
+        c.ibm_kappa = cfg.ibm_kappa
         h = ct.c_void_p()
         check(lib.avz_plan_create(ct.byref(h), ct.byref(c)), "avz_plan_create")
         self._h = h
@@ -113,6 +117,23 @@ class MVDRPlan:
         mode = (2 if analysis_only else 1) if enable else 0
         check(lib.avz_plan_set_timing_period(self._h, int(period)), "avz_plan_set_timing_period")
         check(lib.avz_plan_set_timing(self._h, mode), "avz_plan_set_timing")
+
+    def set_ibm_stats(self, counts) -> None:
+        """Diagnostics of the exact IBM path: every later run() adds to counts[0] the frames
+        and to counts[1] the (bin, frame) decisions taken there (a zeroed int64 CUDA tensor of
+        2 elements; None = off)."""
+        if counts is not None:
+            assert counts.dtype == torch.int64 and counts.is_cuda and counts.numel() >= 2
+        check(lib.avz_plan_set_ibm_stats(self._h, _ptr(counts)), "avz_plan_set_ibm_stats")
+        self._ibm_stats = counts  # keep the buffer alive
+
+    def set_diagnostics(self, synth_variant: int = 2, ipf_mode: int = 0) -> None:
+        """Kernel-path A/B of this plan's later runs (tests / tools; include/avz.h
+        avz_plan_set_diagnostics): synth_variant 2 = per-utterance synthesis solving its own
+        bins (default), 1 = after the solve kernel, 0 = chunk grid + finalize; ipf_mode 1 / 2
+        force the in-kernel piece finalize's rare paths."""
+        check(lib.avz_plan_set_diagnostics(self._h, int(synth_variant), int(ipf_mode)),
+              "avz_plan_set_diagnostics")
 
     def timing(self) -> dict:
         """Average ms per kernel over the runs since set_timing(True) (waits for them;

@@ -31,6 +31,8 @@ struct Workspace {
   float* ptails;
   int seam_slots;
   avz::PieceState* pstate;   // [batch] in-kernel piece finalize: arrivals, 1/peak, hand-backs
+  uint32_t* xpend;           // IBM plans: [units][4] exact-path records (ChainArgs)
+  uint32_t* xdfr;            // IBM plans: [units][F] per-bin deferrals
 };
 
 // Tail-splitting capacity (ChainArgs a_* / s_*): analysis pieces of a partial last round
@@ -59,6 +61,11 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
   const int ts = tail_slots(B, nchunk), ss = seam_slots(B, nchunk);
   const size_t sz_tpart = align256(sizeof(float) * (size_t)ts * 5 * F);
   const size_t sz_seam = align256(sizeof(float) * (size_t)ss * H);
+  // exact IBM path: one record per analysis unit (whole items + tail pieces)
+  const long long units = c.mask_mode == AVZ_MASK_IBM ? B * nchunk + ts : 0;
+  const size_t sz_xp = align256(sizeof(uint32_t) * 4 * units);
+  const size_t sz_xd = align256(sizeof(uint32_t) * (size_t)F * units);
+
   if (base && w) {
     char* q = base;
     w->part = reinterpret_cast<float*>(q); q += sz_part;
@@ -76,8 +83,11 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
     w->ptails = reinterpret_cast<float*>(q); q += sz_seam;
     w->seam_slots = ss;
     w->pstate = reinterpret_cast<avz::PieceState*>(q); q += 4 * sz_b;
+    w->xpend = units ? reinterpret_cast<uint32_t*>(q) : nullptr; q += sz_xp;
+    w->xdfr = units ? reinterpret_cast<uint32_t*>(q) : nullptr; q += sz_xd;
   }
-  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 6 * sz_b + sz_gain + sz_tpart + 2 * sz_seam;
+  return sz_part + sz_mw + sz_coef + 2 * sz_ht + 6 * sz_b + sz_gain + sz_tpart + 2 * sz_seam +
+         sz_xp + sz_xd;
 }
 
 struct avz_plan {
@@ -85,8 +95,14 @@ struct avz_plan {
   double tau1, tau2;         // far-field delays of the two mics (masked_mvdr.py:28-29)
   int max_frames;
   int nchunk;                // 32-frame chunks of a max_samples utterance
-  void* arena;               // steering table + the plan's own workspace
+  void* arena;               // steering table, exact-IBM tables + the plan's own workspace
   double* steer;             // [F][4] steering vectors (masked_mvdr.py:22-35), fp64
+  double* xtw;               // [N][2] W_N^j, fp64 (exact IBM path)
+  float* xwin;               // [N] the reference's fp32 Hann window (exact IBM path)
+  float ibm_cert;            // ibm_kappa * 2^-24 (0: no certificate)
+  unsigned long long* xstat; // avz_plan_set_ibm_stats (diagnostic) or null
+  int synth_variant;         // avz_plan_set_diagnostics (default 2)
+  int dbg_ipf;               // avz_plan_set_diagnostics (default 0)
   Workspace ws;              // used by calls that pass no workspace (serialised by contract)
   // diagnostic per-kernel timing (avz_plan_set_timing): two event sets used alternately
   bool timing;
@@ -133,7 +149,7 @@ static int hip_fail(hipError_t e) {
   return AVZ_ERR_HIP;
 }
 
-extern "C" int avz_version(void) { return 2; }
+extern "C" int avz_version(void) { return 3; }
 
 extern "C" const char* avz_last_hip_error(void) { return g_last_hip.c_str(); }
 
@@ -154,6 +170,28 @@ static bool misaligned(const void* ptr, uintptr_t bytes) {
 }
 
 static int frames_for(int len, int hop) { return (len + hop - 1) / hop + 1; }
+
+// scipy.signal.get_window('hann', n) cast to float32 (the reference's STFT window,
+// _spectral_py.py:2083-2084): 0.5 + 0.5 cos(fac), fac = np.linspace(-pi, pi, n + 1)[:-1]
+// evaluated as numpy does (i * step, then + start; no fused multiply-add).
+#pragma clang fp contract(off)
+static void ref_window_f32(int n, float* out) {
+  const double start = -M_PI, step = (M_PI - start) / n;
+  for (int i = 0; i < n; ++i) {
+    double y = (double)i * step;
+    y = y + start;
+    const double c = std::cos(y);
+    const double w = 0.5 + 0.5 * c;
+    out[i] = (float)w;
+  }
+}
+#pragma clang fp contract(on)
+
+extern "C" int avz_ibm_window(int n, float* out) {
+  if ((n != 512 && n != 1024) || !out) return AVZ_ERR_ARG;
+  ref_window_f32(n, out);
+  return AVZ_OK;
+}
 
 extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
   if (!out || !cfg) return AVZ_ERR_ARG;
@@ -190,16 +228,36 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
   const int F = c.n_fft / 2 + 1;
   {
     p->nchunk = (p->max_frames + avz_chunk_frames() - 1) / avz_chunk_frames();
+    const int N = c.n_fft;
     const size_t sz_steer = align256(sizeof(double) * F * 4);
+    const size_t sz_xtw = align256(sizeof(double) * N * 2), sz_xwin = align256(sizeof(float) * N);
+    const size_t sz_tab = sz_steer + sz_xtw + sz_xwin;
     const size_t sz_ws = ws_layout(c, c.max_batch, p->nchunk, nullptr, nullptr);
-    hipError_t e = hipMalloc(&p->arena, sz_steer + sz_ws);
+    hipError_t e = hipMalloc(&p->arena, sz_tab + sz_ws);
     if (e != hipSuccess) {
       delete p;
       return hip_fail(e);
     }
     char* q = static_cast<char*>(p->arena);
     p->steer = reinterpret_cast<double*>(q);
-    ws_layout(c, c.max_batch, p->nchunk, q + sz_steer, &p->ws);
+    p->xtw = reinterpret_cast<double*>(q + sz_steer);
+    p->xwin = reinterpret_cast<float*>(q + sz_steer + sz_xtw);
+    ws_layout(c, c.max_batch, p->nchunk, q + sz_tab, &p->ws);
+    const double kappa = c.ibm_kappa == 0.0 ? AVZ_IBM_KAPPA : c.ibm_kappa;
+    p->ibm_cert = kappa > 0.0 ? (float)(kappa * 0x1p-24) : 0.0f;
+    p->xstat = nullptr;
+    p->synth_variant = 2;
+    p->dbg_ipf = 0;
+    // exact IBM path: W_N^j = exp(-2 pi i j / N) (long double argument, rounded once) and the
+    // reference's fp32 window
+    std::vector<double> xt((size_t)N * 2);
+    for (int j = 0; j < N; ++j) {
+      const long double a = -2.0L * 3.141592653589793238462643383279502884L * j / N;
+      xt[2 * j] = (double)cosl(a);
+      xt[2 * j + 1] = (double)sinl(a);
+    }
+    std::vector<float> xw((size_t)N);
+    ref_window_f32(N, xw.data());
     // d_m(f_k) = exp(-1j * (2 pi f_k) * tau_m), f_k = np.fft.rfftfreq(n_fft, 1/fs)[k]
     // (masked_mvdr.py:22-35); the hybrid null beamformer phase-normalises it to mic 0,
     // v / (v[0] + 1e-10) (Final_pipeline/src/inference.py:16-26).
@@ -221,6 +279,10 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
       st[4 * k + 3] = d1.imag();
     }
     e = hipMemcpy(p->steer, st.data(), sizeof(double) * st.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(p->xtw, xt.data(), sizeof(double) * xt.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = hipMemcpy(p->xwin, xw.data(), sizeof(float) * xw.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       (void)hipFree(p->arena);
       delete p;
@@ -280,6 +342,12 @@ static void plan_params(const avz_plan* p, avz::ChainArgs& k) {
   k.bypass_hz = c.bypass_hz;
   k.cond_max = c.cond_max;
   k.steer = p->steer;
+  k.ibm_cert = p->ibm_cert;
+  k.xwin = p->xwin;
+  k.xtw = p->xtw;
+  k.xstat = p->xstat;
+  k.synth_variant = p->synth_variant;
+  k.dbg_ipf = p->dbg_ipf;
 }
 
 enum { USE_CHAIN = 0, USE_COVARIANCE = 1, USE_APPLY = 2 };
@@ -357,6 +425,8 @@ static int prepare_chain(const avz_plan* p, const avz_batch_args* a, int use, av
   k.ptails = ws.ptails;
   k.pseam_slots = ws.seam_slots;
   k.pstate = ws.pstate;
+  k.xpend = ws.xpend;
+  k.xdfr = ws.xdfr;
   if (use == USE_COVARIANCE) {  // that stage produces cov_out only: leave the caller's
     k.out = nullptr;            // out / peak / w buffers untouched (the analysis kernel
     k.peak = nullptr;           // would otherwise zero peak[b] as the atomicMax target)
@@ -539,6 +609,21 @@ extern "C" int avz_plan_set_timing(avz_plan* p, int enable) {
       }
     }
   p->timing = true;
+  return AVZ_OK;
+}
+
+extern "C" int avz_plan_set_ibm_stats(avz_plan* p, unsigned long long* counts) {
+  if (!p) return AVZ_ERR_ARG;
+  if (misaligned(counts, 8)) return AVZ_ERR_ALIGN;
+  p->xstat = counts;
+  return AVZ_OK;
+}
+
+extern "C" int avz_plan_set_diagnostics(avz_plan* p, int synth_variant, int ipf_mode) {
+  if (!p || synth_variant < 0 || synth_variant > 2 || ipf_mode < 0 || ipf_mode > 2)
+    return AVZ_ERR_ARG;
+  p->synth_variant = synth_variant;
+  p->dbg_ipf = ipf_mode;
   return AVZ_OK;
 }
 

@@ -4,7 +4,11 @@
 #include "avz_chunked_inst.hpp"
 
 namespace avz {
+#ifdef AVZ_ONE_TU  // diagnostic: every kernel compiled in this unit (the pre-split build)
+#define AVZ_INST template
+#else
 #define AVZ_INST extern template
+#endif
 AVZ_ANALYSIS_INST(1024)
 AVZ_ANALYSIS_INST(512)
 AVZ_UTT_INST
@@ -19,22 +23,6 @@ extern "C" int avz_chunk_frames(void) { return kChunk; }
 
 static int resident_cus();
 
-// Synthesis kernel selection (diagnostic A/B, avz_debug_set_synth_variant): 1 = the
-// per-utterance kernel for N = 1024 time-domain input (no finalize launch), 0 = the
-// two-block chunk kernel + avz_finalize_kernel.
-static std::atomic<int> g_synth_variant{2};
-// In-kernel piece finalize's rare paths forced (tests): ChainArgs::dbg_ipf.
-static std::atomic<int> g_dbg_ipf{0};
-extern "C" int avz_debug_set_ipf_mode(int m) {
-  if (m < 0 || m > 2) return -1;
-  g_dbg_ipf.store(m);
-  return 0;
-}
-extern "C" int avz_debug_set_synth_variant(int v) {
-  if (v < 0 || v > 2) return -1;
-  g_synth_variant.store(v);
-  return 0;
-}
 // The per-utterance kernel covers the IBM-target and unfiltered post-filters (the headline
 // and the IPD configuration); the IRM and external-mask gains, read per (bin, frame) from
 // memory, need registers it does not have (48-56 B of scratch), so those plans keep the
@@ -48,13 +36,13 @@ template <int N, int PF, bool SPEC>
 static bool synth_per_utterance(const ChainArgs* a) {
   return (N == 1024 || (N == 512 && a->batch % resident_cus() == 0)) && !SPEC &&
          (PF == PF_IBM_TARGET || PF == PF_NONE) && a->normalize == NORM_PEAK &&
-         g_synth_variant.load(std::memory_order_relaxed) >= 1;
+         a->synth_variant >= 1;
 }
 // ... and solves the utterance's bins itself (variant 2) when the chain's solve is the plain
 // MVDR one: no item-level fallback flags, no covariance / weight debug outputs.
 template <int N, int PF>
 static bool solve_fused(const ChainArgs* a) {
-  return synth_per_utterance<N, PF, false>(a) && g_synth_variant.load(std::memory_order_relaxed) == 2 &&
+  return synth_per_utterance<N, PF, false>(a) && a->synth_variant == 2 &&
          a->beamformer == BF_MVDR && a->singular_fallback != 2 && !a->cov_out && !a->w_out &&
          !a->cov_only;
 }
@@ -134,7 +122,6 @@ static int launch_synth_finalize(const ChainArgs* a0, hipStream_t st, const hipE
       c.s_pieces = sp.pieces;
       c.s_steps = sp.steps;
       c.s_ipf = sp.ipf ? 1 : 0;
-      c.dbg_ipf = g_dbg_ipf.load(std::memory_order_relaxed);
       grid = dim3((unsigned)sp.grid);
     }
     if constexpr (N == 1024) {

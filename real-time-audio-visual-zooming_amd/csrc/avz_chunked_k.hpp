@@ -30,6 +30,13 @@
 #include <type_traits>
 
 #include "avz_common.hpp"
+#include "avz_ibm_exact.hpp"
+#ifndef AVZ_NO_IBM_CERT  // diagnostic build: no certificate in the reference-bit path
+#define AVZ_NO_IBM_CERT 0
+#endif
+#ifndef AVZ_CERT_PARTS  // diagnostic: bit 0 frame energy, bit 1 per-bin test, bit 2 min form
+#define AVZ_CERT_PARTS 7
+#endif
 
 namespace avz {
 
@@ -151,6 +158,31 @@ __device__ __forceinline__ void window_apply(cf (&v)[PPL], float a0, float ac, f
   });
 }
 
+// IBM decision |S_int| > |S_tgt| (oracle_debug.py:49-53, strict) from the packed reference
+// pair z = tgt + i int: 2T = zr + conj(zrp), 2I = (zr - conj zrp)/i, and
+// |2T|^2 - |2I|^2 = 4 Re(zr zrp), so noise <=> Re(zr zrp) < 0 (one product, one fma).
+__device__ __forceinline__ bool ibm_noise(cf zr, cf zrp) {
+  return fmaf(zr.x, zrp.x, -(zr.y * zrp.y)) < 0.0f;
+}
+
+// Sum over the 32 lanes of a lane group (DPP within rows, v_permlane16_swap across them).
+__device__ __forceinline__ float group32_sum(float e) {
+  e += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(e), 0xB1, 0xF, 0xF, false));
+  e += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(e), 0x4E, 0xF, 0xF, false));
+  e += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(e), 0x141, 0xF, 0xF, false));
+  e += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(e), 0x140, 0xF, 0xF, false));
+  float lo, hi;
+  xhalf<16>(e, lo, hi);
+  return lo + hi;
+}
+__device__ __forceinline__ float frame_energy(const cf (&v)[32]) {
+  float e = 0.0f;
+  static_for<0, 32>([&](auto r) {
+    e = fmaf(v[r].x, v[r].x, e);
+    e = fmaf(v[r].y, v[r].y, e);
+  });
+  return e;
+}
 // Window + forward FFT with the lane's twiddles in registers (N = 1024 analysis). Both
 // FFT stages store each output pair as it is formed (the transpose scratch, then the
 // spectrum); after(k) runs right after spectrum output k is stored (the next step's load
@@ -159,12 +191,15 @@ struct NoAfter {
   template <class K>
   __device__ __forceinline__ void operator()(K) const {}
 };
+// en (non-null: IBM reference waves of the plans without the reference-bit hand-off): the
+// group's windowed frame energy, the exact-IBM certificate's scale (ibm_exact_frames).
 template <class After = NoAfter>
 __device__ __forceinline__ void window_fft_reg(cf (&v)[32], const WinCoef<1024>& wc,
                                                const Fft1024x2& fft, cf* spec,
                                                const cf (&tw_reg)[31], const LaneMap<1024>& lm,
-                                               After&& after = After{}) {
+                                               After&& after = After{}, float* en = nullptr) {
   window_apply(v, wc.a0, wc.ac, wc.as);
+  if (en) *en = group32_sum(frame_energy(v));
   fft.stage1_reg_st(v, spec, tw_reg);
   fft.transpose_read(v, spec);
   fft.stage2_emit(v, [&](auto k, cf x) {
@@ -182,11 +217,26 @@ __device__ __forceinline__ void window_fft_reg(cf (&v)[32], const WinCoef<1024>&
 // slot (bytes 0..127) and only then reloads registers 0-15 (analysis 80.7-80.9 -> 79.1-79.5
 // us against storing all 32 and reading both operands back, profiles/r04/ab_ref_half.txt).
 // The Nyquist bin (lane 0, k = 16) stays readable at spec[N / 2].
+//
+// Certificate (avz_ibm_exact.hpp): the group's windowed frame energy gives delta = cert
+// ||z|| (cert = kappa eps, ChainArgs::ibm_cert), a bound on every output bin's error; a bin
+// pair whose |Re(Zr[k] Zr[N - k])| does not clear (2 sqrt 2 + 1) delta max(|components|,
+// delta) could be decided either way by that error. A frame with such a bin (DC included)
+// publishes no noise bits and returns true: the item's exact path decides it
+// (ibm_exact_item). delta goes to dl; the Nyquist bin (lane 0, k = 16, left in spec[N / 2])
+// is certified by the bin phase's Nyquist wave with it.
+// true when the pair's decision is not certified by the error bound dl (= delta)
+__device__ __forceinline__ bool ibm_uncertain(cf zr, cf zrp, float dl) {
+  const float d = fmaf(zr.x, zrp.x, -(zr.y * zrp.y));
+  const float m = fmaxf(fmaxf(fabsf(zr.x), fabsf(zr.y)), fmaxf(fmaxf(fabsf(zrp.x), fabsf(zrp.y)), dl));
+  return fabsf(d) < 3.9f * dl * m;
+}
 template <class After = NoAfter>
-__device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCoef<1024>& wc,
+__device__ __forceinline__ bool window_fft_reg_ibm_bits(cf (&v)[32], const WinCoef<1024>& wc,
                                                         const Fft1024x2& fft, cf* spec,
                                                         const cf (&tw_reg)[31],
-                                                        const LaneMap<1024>& lm,
+                                                        const LaneMap<1024>& lm, float eg0,
+                                                        float eg1, float cert, float& dl,
                                                         After&& after = After{}) {
   constexpr int N = 1024;
   window_apply(v, wc.a0, wc.ac, wc.as);
@@ -199,16 +249,41 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
       after(k);
     }
   });
+  dl = cert * sqrtf(lm.grp ? eg1 : eg0);  // delta >= kappa eps ||z|| (the caller's scale)
   __builtin_amdgcn_wave_barrier();
+  // the word is built from bit 15 down (w = 2 w + bit): a select of 1 << k per bin held the
+  // 16 constants in VGPRs for the whole kernel
   uint32_t w = 0u;
-  static_for<0, 16>([&](auto k) {
+  bool unc = false;
+  float slack = __builtin_inff();  // min over bins of |D| - 3.9 dl m (< 0: uncertain)
+  const float dl39 = 3.9f * dl;
+  static_for<0, 16>([&](auto kk) {
+    constexpr int k = 15 - decltype(kk)::value;
     const int m = l + 32 * k;
     cf zp = spec[(N - m) & (N - 1)];
     if (k == 0 && l == 0) zp = v[0];  // DC: its own partner (index 0 is not stored)
-    w |= (ibm_noise(v[k], zp) ? 1u : 0u) << k;
+    w = (w << 1) | (ibm_noise(v[k], zp) ? 1u : 0u);
+    if (!AVZ_NO_IBM_CERT && (AVZ_CERT_PARTS & 2)) {
+      if (AVZ_CERT_PARTS & 4) {
+        const float d = fmaf(v[k].x, zp.x, -(v[k].y * zp.y));
+        const float mm = fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)),
+                               fmaxf(fmaxf(fabsf(zp.x), fabsf(zp.y)), dl));
+        slack = fminf(slack, fmaf(-dl39, mm, fabsf(d)));
+      } else {
+        unc |= ibm_uncertain(v[k], zp, dl);
+      }
+    }
   });
+  if (AVZ_CERT_PARTS & 4) unc = slack < 0.0f;
+  const unsigned long long ub = __ballot(unc);
+  bool defer = false;
+  if (ub != 0ull) {  // rare (wave-uniform)
+    defer = ((ub >> (32 * lm.grp)) & 0xffffffffull) != 0ull;
+    if (defer) w = 0u;
+  }
   reinterpret_cast<uint32_t*>(spec)[l] = w;
   static_for<0, 16>([&](auto k) { after(k); });
+  return defer;
 }
 
 // Window + forward FFT of the synthesis kernel and of the N = 512 analysis kernel:
@@ -219,13 +294,22 @@ __device__ __forceinline__ void window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
 template <int N, bool IL512 = false, class After = NoAfter>
 __device__ __forceinline__ void window_fft(cf (&v)[KCfg<N>::PPL], const WinCoef<N>& wc,
                                            const typename KCfg<N>::Fft& fft, cf* spec,
-                                           const LaneMap<N>& lm, After&& after = After{}) {
+                                           const LaneMap<N>& lm, After&& after = After{},
+                                           float* en = nullptr) {
   using C = KCfg<N>;
   float a0 = wc.a0, ac = wc.ac, as = wc.as;
   opaque(a0);
   opaque(ac);
   opaque(as);
   window_apply<N>(v, a0, ac, as);
+  if (en) {  // the lane group's windowed frame energy (exact-IBM certificate scale)
+    float e = 0.0f;
+    static_for<0, C::PPL>([&](auto r) {
+      e = fmaf(v[r].x, v[r].x, e);
+      e = fmaf(v[r].y, v[r].y, e);
+    });
+    *en = group32_sum(e);
+  }
   if constexpr (N == 1024) {
     fft.stage1_ab_st(v, spec);
     fft.transpose_read(v, spec);
@@ -297,18 +381,12 @@ __device__ __forceinline__ void store_through(float* row, int n, int i, float4 v
 // len[] is read-only for the whole chain, so it is read through the constant address space:
 // with a wave-uniform b that is one s_load_dword (scalar cache) instead of a vector load
 // plus readfirstlane on the item / unit start's dependent latency chain.
-__device__ __forceinline__ int utt_len(const ChainArgs& A, int b) {
+template <class CA>
+__device__ __forceinline__ int utt_len(CA& A, int b) {
   if (!A.len) return A.max_len;
   const __attribute__((address_space(4))) int* lc =
       (const __attribute__((address_space(4))) int*)(A.len);
   return min(lc[b], A.max_len);
-}
-
-// IBM decision |S_int| > |S_tgt| (oracle_debug.py:49-53, strict) from the packed reference
-// pair z = tgt + i int: 2T = zr + conj(zrp), 2I = (zr - conj zrp)/i, and
-// |2T|^2 - |2I|^2 = 4 Re(zr zrp), so noise <=> Re(zr zrp) < 0 (one product, one fma).
-__device__ __forceinline__ bool ibm_noise(cf zr, cf zrp) {
-  return fmaf(zr.x, zrp.x, -(zr.y * zrp.y)) < 0.0f;
 }
 
 // Mask value m and covariance weight of one (bin, frame).
@@ -345,14 +423,244 @@ __device__ __forceinline__ float irm_gain(cf zr, cf zrp) {
 }
 
 // ================================ analysis ================================
+// The kernel's ChainArgs read afresh from the kernarg segment through an opaque address:
+// fields only the exact path uses were otherwise loaded at the kernel's start and held
+// through the step loop (12 SGPRs more, spilled into VGPR lanes).
+// In the constant address space: its fields are scalar loads (uniform). Through a generic
+// pointer they were vector loads the compiler took for divergent: every buffer load of the
+// exact path then ran in a descriptor waterfall loop.
+using KArgs = const __attribute__((address_space(4))) ChainArgs;
+__device__ __forceinline__ KArgs& kernarg_chain_args() {
+  uintptr_t u = (uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(u));
+  return *(KArgs*)u;
+}
 struct NoTw {};
+using Tw1024 = cf[31];  // the register-twiddle path's twiddles (a type tag here)
+// Exact-phase LDS layout (after the persistent loop; nothing of the loop's is live): the
+// waves' fp64 transform buffers, then (same bytes, after a barrier) the round's mic spectra in
+// frame slots 0-3; the round's reference magnitudes; the fp64 twiddle table. The fp32
+// twiddle table (TW_OFF, the mic transforms') is kept.
+// The round's frames packed one per byte (0xff: none): frame i, or -1, for a block- or
+// lane-varying i by shifts (an int array indexed so went to scratch memory, selects included)
+__device__ __forceinline__ int pick(uint32_t packed, int i) {
+  return (int)(signed char)(packed >> (8 * i));
+}
+template <int N>
+struct XLds {
+  using C = KCfg<N>;
+  using X = XGeo<N>;
+  static constexpr int FR = 4;                              // frames per round
+  static constexpr int MP = N / 2 + 4;                      // magnitude row (16-B aligned)
+  static constexpr int MIC_BYTES = FR / C::FPW * C::WAVE_BYTES;
+  static constexpr int MAG_OFF = (4 * X::SCRATCH > MIC_BYTES) ? 4 * X::SCRATCH : MIC_BYTES;
+  static constexpr int TWL_OFF = MAG_OFF + 2 * FR * MP * 4;
+  static constexpr int WIN_OFF = TWL_OFF + (N / 2) * 16;    // fp32 window [N]
+  static constexpr int SLOT_OFF = WIN_OFF + N * 4;           // XSlot[FR], the round's frames
+  static constexpr int SCAN_OFF = SLOT_OFF + FR * 32;       // int[256]: the deferral scan
+  static constexpr int WL = 32;                             // frames one block decides
+  static constexpr int WL_OFF = SCAN_OFF + 256 * 4;         // int4[WL]: (unit, f, e, -)
+  static constexpr int CTL_OFF = WL_OFF + WL * 16;          // int[8]: counts, mode
+  static constexpr int END = CTL_OFF + 32;
+  static_assert(C::FPW == 2 && END <= CGeo<N>::SLOT_LDS, "exact phase LDS");
+};
+
+// One deferred frame of the exact path (block-uniform, in LDS): analysis unit, chunk frame f,
+// (e: unused), utterance b and length L, chunk c,
+// flags bit 0: the frame deferred whole (reference-bit path), bit 1: its Nyquist bin deferred.
+struct XSlot {
+  int unit, f, e, b, L, c, flags, pad;
+};
+// slot g's fields as block-uniform scalars (read from LDS they are VGPRs to the compiler: the
+// descriptors built from them put every buffer load in a waterfall loop)
+__device__ __forceinline__ XSlot slot_u(const XSlot* sl, int g) {
+  const XSlot v = sl[g];
+  XSlot s;
+  s.unit = __builtin_amdgcn_readfirstlane(v.unit);
+  s.f = __builtin_amdgcn_readfirstlane(v.f);
+  s.e = 0;
+  s.b = __builtin_amdgcn_readfirstlane(v.b);
+  s.L = __builtin_amdgcn_readfirstlane(v.L);
+  s.c = __builtin_amdgcn_readfirstlane(v.c);
+  s.flags = __builtin_amdgcn_readfirstlane(v.flags);
+  s.pad = 0;
+  return s;
+}
+// The analysis unit u's item: whole items u < n_items (b = u / gx, c = u % gx), tail pieces
+// n_items + q (item n_whole + q / P); its partials (chunk partials / the piece's tail slot).
+template <int F, class CA>
+__device__ __forceinline__ float* unit_item(CA& A, int u, int gx, int n_items, int n_whole, int P,
+                                            int& b, int& c) {
+  if (u < n_items) {
+    b = u / gx;
+    c = u % gx;
+    return A.part + ((long long)b * A.nchunk + c) * 5 * F;
+  }
+  const int q = u - n_items, it = n_whole + q / P;
+  b = it / gx;
+  c = it % gx;
+  return A.tpart + (long long)q * 5 * F;
+}
+
+// Reference-exact decisions of up to four deferred frames of one unit (avz_ibm_exact.hpp): wave w forms
+// the fp64 spectra (ref_spectrum_exact) of reference w & 1 (target / interference) of slots
+// w / 2 and w / 2 + 2 -- sample loads first --, waves 0-1 the slots' mic spectra, then thread
+// per bin decides |I| > |T| for the slot's deferred bins (the whole frame below N/2, or the
+// bins of xdfr[unit][k]; the Nyquist bin when flagged) and adds the frame's covariance terms
+// and noise bit to the caller's running sums, in slot (= frame) order.
+// After the loop, not in it: inlined at the item's end the step loop's kernels (248-253 of
+// 256 VGPRs) spilled 105+ VGPRs; here nothing of the loop is live.
+template <int N, bool PER_BIN>
+__device__ __forceinline__ void exact_round(KArgs& A, unsigned char* lds, const XSlot* sl, int ns,
+                                            Acc32 (&pacc)[CGeo<N>::BPT + 1],
+                                            uint32_t (&pbits)[CGeo<N>::BPT + 1]) {
+  using C = KCfg<N>;
+  using G = CGeo<N>;
+  using X = XGeo<N>;
+  using XL = XLds<N>;
+  constexpr int NT = G::NT, H = G::H, F = G::F, BPT = G::BPT, PPL = C::PPL, MP = XL::MP;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  float* const mag = reinterpret_cast<float*>(lds + XL::MAG_OFF);  // [2 FR][MP]
+  const cd* const twl = reinterpret_cast<const cd*>(lds + XL::TWL_OFF);
+  const float* const win = reinterpret_cast<const float*>(lds + XL::WIN_OFF);
+  cd* const buf = reinterpret_cast<cd*>(lds + wave * X::SCRATCH);
+  AVZ_STAMP_DECL();
+  AVZ_STAMP_INIT();
+  // lane-derived addresses formed here (hoisted out of the caller's loop they spilled)
+  int lane_o = lane;
+  opaque_i(lane_o);
+  // the wave's two reference frames and (waves 0-1) the mic frames, loads first
+  const int ga = wave >> 1, gb = (wave >> 1) + 2;
+  const float* const refp = (wave & 1) ? A.ref_int : A.ref_tgt;
+  float xa[N / 64], xb[N / 64];
+  if (ga < ns) {
+    const XSlot s = slot_u(sl, ga);
+    ref_frame_load<N>(make_rsrc(refp + (long long)s.b * A.ref_stride, s.L),
+                      (s.c * kChunk + s.f) * H - N / 2, lane_o, xa);
+  }
+  if (gb < ns) {
+    const XSlot s = slot_u(sl, gb);
+    ref_frame_load<N>(make_rsrc(refp + (long long)s.b * A.ref_stride, s.L),
+                      (s.c * kChunk + s.f) * H - N / 2, lane_o, xb);
+  }
+  if (ga < ns) ref_spectrum_exact<N>(xa, twl, win, buf, mag + (2 * ga + (wave & 1)) * MP, lane_o);
+  AVZ_STAMP(4);
+  // waves 0-1: the mic frames' loads (one slot per lane group), in flight through the second
+  // transform
+  cf v[PPL];
+  LaneMap<N> lm;
+  lm.init(lane_o);
+  const int gm = C::FPW * wave + lm.grp;
+  if (wave < XL::FR / C::FPW) {
+    // the round's slots are frames of one unit (one utterance): one descriptor pair, the
+    // lane group's frame in the offset
+    const XSlot s = slot_u(sl, 0);
+    const float* mixb = A.mix + (long long)s.b * A.mix_stride;
+    const rsrc_t r_m0 = make_rsrc(mixb, s.L), r_m1 = make_rsrc(mixb + A.ch_stride, s.L);
+    const bool on = gm < ns;
+    const int fm = sl[on ? gm : 0].f;
+    const int s0 = (s.c * kChunk + fm) * H - N / 2 + lm.in0;
+#pragma unroll
+    for (int r = 0; r < PPL; ++r) {
+      v[r].x = on ? bload(r_m0, s0 + C::IN_STRIDE * r) : 0.0f;
+      v[r].y = on ? bload(r_m1, s0 + C::IN_STRIDE * r) : 0.0f;
+    }
+  }
+  if (gb < ns) {
+    int lane_b = lane;
+    opaque_i(lane_b);
+    ref_spectrum_exact<N>(xb, twl, win, buf, mag + (2 * gb + (wave & 1)) * MP, lane_b);
+  }
+  AVZ_STAMP(5);
+  lds_barrier();  // the transform buffers are the mic spectra's slots
+  AVZ_STAMP(6);
+  if (wave < XL::FR / C::FPW) {  // the mic spectra (zeros for an absent slot)
+    WinCoef<N> wc;
+    wc.init(lm);
+    cf* const spec = slot_ptr<N>(lds, gm);
+    if constexpr (N == 1024) {
+      // the unrotated frame on the LDS twiddle table: the step's register twiddles (and the
+      // pair loads' rotation) stay out of this phase, whose registers they would hold
+      Fft1024x2 f;
+      f.l = lm.out0;
+      window_apply(v, wc.a0, wc.ac, wc.as);
+      f.forward(v, spec, reinterpret_cast<const cf*>(lds + G::TW_OFF));
+      static_for<0, 32>([&](auto k) { spec[lm.out0 + 32 * k] = v[k]; });
+    } else {
+      Fft512x2 f;
+      f.init(lane_o);
+      window_fft<N>(v, wc, f, spec, lm);
+    }
+  }
+  AVZ_STAMP(7);
+  lds_barrier();
+  AVZ_STAMP(8);
+  // decisions |I| > |T| and the frames' covariance terms, thread per bin as the step's,
+  // onto the caller's running sums (one unit's frames, in frame order)
+  unsigned long long n_exact = 0;
+  for (int g = 0; g < ns; ++g) {  // block-uniform
+    const XSlot s = slot_u(sl, g);
+    const cf* Zm = slot_ptr<N>(lds, g);
+    auto put = [&](int j, int k, const Acc32& a, bool dfr, bool noise) {
+      if (dfr) {
+        pacc[j].c00 += a.c00;
+        pacc[j].c11 += a.c11;
+        pacc[j].c01r += a.c01r;
+        pacc[j].c01i += a.c01i;
+        pacc[j].cm += a.cm;
+        pbits[j] |= (noise ? 1u : 0u) << s.f;
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int kb = tid + j * NT;
+      const int kp = (N - kb) & (N - 1);
+      const bool dfr = PER_BIN ? ((A.xdfr[(long long)s.unit * F + kb] >> s.f) & 1u) : (s.flags & 1);
+      Acc32 a;
+      a.zero();
+      bool noise = false;
+      if (dfr) {
+        noise = mag[(2 * g + 1) * MP + kb] > mag[(2 * g) * MP + kb];
+        cf x0, x1;
+        split_pair2(Zm[kb], Zm[kp], x0, x1);
+        a.add_sel(x0, x1, noise);
+        a.cm = noise ? 1.0f : 0.0f;
+        n_exact += 1;
+      }
+      put(j, kb, a, dfr, noise);
+    }
+    if (tid == NT - 1) {  // the Nyquist bin
+      const bool dfr = (s.flags >> 1) & 1;
+      Acc32 a;
+      a.zero();
+      bool noise = false;
+      if (dfr) {
+        noise = mag[(2 * g + 1) * MP + N / 2] > mag[(2 * g) * MP + N / 2];
+        cf y0, y1;
+        split_pair2(Zm[N / 2], Zm[N / 2], y0, y1);
+        const float wn = noise ? 1.0f : 0.0f;
+        a.add(y0, y1, wn, wn);
+        n_exact += 1;
+      }
+      put(BPT, N / 2, a, dfr, noise);
+    }
+  }
+  if (A.xstat && n_exact) atomicAdd(A.xstat + 1, n_exact);  // diagnostic: decisions
+  AVZ_STAMP(9);
+  lds_barrier();
+  AVZ_STAMP(10);
+}
+
+
 // piece p of P (P = 1: the whole item) runs the chunk's steps [p SA / P, (p + 1) SA / P), SA =
 // steps per chunk; slot >= 0: its partials go to tail slot `slot` of tpart and its IBM bits
 // into the chunk's mask words atomically (the other pieces own the word's other bits).
+// seq: the block's item count (parity of the IBM pending-frame word, see pendw).
 template <int N, int MASK, bool IRM, class TW>
 __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char* lds, int c,
                                               int b, int p, int P, int slot, const TW& tw_reg,
-                                              const LaneConst<N>& K) {
+                                              const LaneConst<N>& K, int seq) {
   using C = KCfg<N>;
   using G = CGeo<N>;
   constexpr int NT = G::NT, H = G::H, F = G::F, NSLOT = G::NSLOT, BPT = G::BPT, PPL = C::PPL;
@@ -365,6 +673,10 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   // (not IPD: its decisions are pinned bit-exact to the reference's, and the rotated
   // transform's rounding moved one of 1.3e5 on the ipd_test golden)
   constexpr bool SHARE = N == 1024 && MASK != MASK_IPD && !std::is_same<TW, NoTw>::value;
+  // IBM without the reference-bit hand-off: the reference waves publish each frame's
+  // certificate scale delta (MISC_OFF + 16: four floats) and the bin phase defers the
+  // uncertified (bin, frame) decisions one by one (dfr)
+  constexpr bool DLT = MASK == MASK_IBM && !REFBITS;
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -383,14 +695,29 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   constexpr int SA = kChunk / FB;  // steps of a full chunk
   const int s_lo = p * SA / P;      // this piece's steps [s_lo, nstep)
   const int nstep = min((nframes + FB - 1) / FB, (p + 1) * SA / P);
+  // IBM: frames (bit = chunk frame) with decisions deferred to the exact path
+  // (ibm_exact_units), OR-ed in LDS by the deciding waves before a step barrier, read after
+  // the item's last one. Two pairs of words used by alternate items: the next item clears its
+  // own before its first barrier, which no thread passes before it has read this item's.
+  uint32_t* const pendw = reinterpret_cast<uint32_t*>(lds + G::MISC_OFF + 32 + 8 * (seq & 1));
+  if (MASK == MASK_IBM && tid == 0) {
+    int z = 0;
+    opaque_i(z);  // formed here (a zero pair held across the items spilled)
+    pendw[0] = (uint32_t)z;  // frames with a deferred decision
+    pendw[1] = (uint32_t)z;  // frames deferred whole (reference-bit path)
+  }
 
   const typename C::Fft fft = K.fft;
-  const LaneMap<N> lm = K.lm;
-  WinCoef<N> wc = K.wc;
-  if (SHARE && lm.grp) {  // rotated frame: window halves swapped
-    wc.ac = -wc.ac;
-    wc.as = -wc.as;
+  // the lane map formed per item from an opaque lane (held across the items from the kernel
+  // start, three of its offsets spilled)
+  LaneMap<N> lm;
+  {
+    int ln = threadIdx.x & 63;
+    opaque_i(ln);
+    lm.init(ln);
   }
+  const float cert_raw = A.ibm_cert * (2.0f / N);  // REFBITS: delta per unit raw norm (2 a0)
+  const WinCoef<N> wc = K.wc;  // SHARE: the rotated frames' (group 1) already swapped
   const int my_slot = wave * C::FPW + lm.grp;
   cf* my_spec = slot_ptr<N>(lds, my_slot);
   // IBM: waves 0-1 transform the mic pair, waves 2-3 the reference pair (wave-uniform)
@@ -458,11 +785,13 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
 
   Acc32 acc[BPT];
   uint32_t bits[BPT];
+  uint32_t dfr[BPT];     // DLT: (bin, frame) decisions deferred to the exact path
   int ipd_clear_n[BPT];  // IPD: frames the cross-product test weighted 1
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
     acc[j].zero();
     bits[j] = 0u;
+    dfr[j] = 0u;
     ipd_clear_n[j] = 0;
   }
   // IRM post-filter gains of this chunk (PF_IRM plans only)
@@ -473,7 +802,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   Acc32 an, adc;  // Nyquist; DC (IPD: weighed on the Nyquist wave, not by lane 0)
   an.zero();
   adc.zero();
-  uint32_t nyq_bits = 0u;
+  uint32_t nyq_bits = 0u, nyq_dfr = 0u;
   // IPD: covariance weight of the main bin loop, 0 on the DC lane (bin tid + 256 j)
   float wone[BPT];
 #pragma unroll
@@ -492,6 +821,17 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
 #endif
     if (live) {
       if constexpr (SHARE) pair_finish(v);
+      // reference-bit path: the two frames' energies (raw samples; the window's maximum 2 a0
+      // scales the bound, cert_raw) as wave-uniform values, so nothing extra stays in VGPRs
+      // through the FFT (from the windowed input or the spectrum the kernel spilled 5-125)
+      float eg0 = (AVZ_CERT_PARTS & 1) ? 0.0f : 1.0f, eg1 = eg0;
+      if constexpr (REFBITS && !AVZ_NO_IBM_CERT && (AVZ_CERT_PARTS & 1)) {
+        if (ref) {
+          const float eg = group32_sum(frame_energy(v));
+          eg0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eg), 0));
+          eg1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eg), 32));
+        }
+      }
       if constexpr (MASK == MASK_IPD) {
         // Bitwise-identical channel samples give bitwise-identical pocketfft spectra in the
         // reference, hence equal angles (weight 0.01) in every bin of the frame; the packed
@@ -510,26 +850,37 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         rn_im = more ? r_im : r_none;
         sp_next = (t0 + (step + 1) * FB + (SHARE ? wave_frame0 : my_frame)) * H - N / 2 + lm.in0;
       }
+      float en = 0.0f;
       if constexpr (!IL_LOADS) {
-        window_fft<N>(v, wc, fft, my_spec, lm);
+        window_fft<N>(v, wc, fft, my_spec, lm, NoAfter{}, (DLT && ref) ? &en : nullptr);
       } else if constexpr (REFBITS) {
         // block-uniform: a chunk's last step issues no loads (analysis 79.7 -> 77.0-78.3 us,
         // profiles/r04/ab_last_step_loads.txt; the other masks' kernels keep the
         // empty-descriptor loads: a second copy of their FFT spills)
+        bool whole = false;
         if (step + 1 < nstep) {
           if (ref)
-            window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm, load_reg);
+            whole = window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm, eg0, eg1, cert_raw, en,
+                                            load_reg);
           else
             window_fft_reg(v, wc, fft, my_spec, tw_reg, lm, load_reg);
         } else {
           if (ref)
-            window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm);
+            whole = window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm, eg0, eg1, cert_raw, en);
           else
             window_fft_reg(v, wc, fft, my_spec, tw_reg, lm);
         }
+        if (whole && (lane & 31) == 0) {  // rare: the frame's decisions are the exact path's
+          atomicOr(pendw, 1u << (step * FB + my_frame));
+          atomicOr(pendw + 1, 1u << (step * FB + my_frame));
+        }
       } else {
-        window_fft_reg(v, wc, fft, my_spec, tw_reg, lm, load_reg);
+        window_fft_reg(v, wc, fft, my_spec, tw_reg, lm, load_reg, (DLT && ref) ? &en : nullptr);
       }
+      // IBM: the reference waves publish each frame's certificate scale delta (the bin phase's
+      // per-bin deferrals, the Nyquist bin's); the reference-bit path returns delta itself
+      if (MASK == MASK_IBM && ref && (lane & 31) == 0)
+        reinterpret_cast<float*>(lds + G::MISC_OFF + 16)[my_frame] = REFBITS ? en : A.ibm_cert * sqrtf(en);
     }
     AVZ_STAMP(3);
     if (!IL_LOADS && step + 1 < nstep) issue_loads(step + 1);
@@ -548,6 +899,14 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     const bool mask_vec = MASK == MASK_EXTERNAL && A.mask_st == 1 && (A.mask_sf & 3) == 0 &&
                           (A.mask_sb & 3) == 0 &&
                           ((reinterpret_cast<uintptr_t>(A.ext_mask) & 15) == 0) && (f0 & 3) == 0;
+    float dlt[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if constexpr (DLT) {  // the step's frames' certificate scales
+      const float4 q = *reinterpret_cast<const float4*>(lds + G::MISC_OFF + 16);
+      dlt[0] = q.x;
+      dlt[1] = q.y;
+      dlt[2] = q.z;
+      dlt[3] = q.w;
+    }
     auto bin_phase = [&](auto full, auto vec) {
       // frames whose LDS reads are batched together
       constexpr int G = FB < 4 ? FB : 4;
@@ -611,10 +970,16 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
               }
               if constexpr (MASK == MASK_IBM) {
                 bool noise;
-                if constexpr (REFBITS)
+                if constexpr (REFBITS) {
                   noise = (zw[i] >> (kb >> 5)) & 1u;
-                else
+                } else {
                   noise = ibm_noise(zr[i], zrp[i]);
+                  if (ibm_uncertain(zr[i], zrp[i], dlt[g0 + i])) {  // rare: the exact path's
+                    noise = false;
+                    dfr[j] |= 1u << (step * FB + g0 + i);
+                    atomicOr(pendw, 1u << (step * FB + g0 + i));
+                  }
+                }
                 bits[j] |= (noise ? 1u : 0u) << (step * FB + g0 + i);
                 acc[j].add_sel(x0, x1, noise);  // weight count: popcount of bits at the end
                 if constexpr (IRM) gain[(step * FB + g0 + i) * F + kb] = irm_gain(zr[i], zrp[i]);
@@ -672,7 +1037,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
       }
     }
     if (nyq_wave) {
-      bool noise = false;
+      bool noise = false, nunc = false;
       if (lane < nvalid) {
         const cf* Zm = slot_ptr<N>(lds, lane);
         cf y0, y1, zr{0, 0};
@@ -681,6 +1046,13 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         float wn;
         float mn = bin_mask<MASK>(A, b, y0, y1, zr, zr, N / 2, f0 + lane, noise, wn);
         if (MASK == MASK_IPD && ((ident_w >> (8 * lane)) & 1ull)) wn = mn = 0.01f;
+        if (MASK == MASK_IBM &&
+            ibm_uncertain(zr, zr, reinterpret_cast<const float*>(lds + G::MISC_OFF + 16)[lane])) {
+          noise = false;  // rare: the exact path's
+          wn = mn = 0.0f;
+          nunc = true;
+          atomicOr(pendw, 1u << (step * FB + lane));
+        }
         an.add(y0, y1, wn, mn);
         if constexpr (MASK == MASK_IPD) {  // DC of frame `lane`
           cf d0, d1;
@@ -693,10 +1065,32 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
       }
       const unsigned long long bal = __ballot(noise);
       nyq_bits |= ((uint32_t)bal & ((1u << FB) - 1u)) << (step * FB);
+      if constexpr (MASK == MASK_IBM)
+        nyq_dfr |= ((uint32_t)__ballot(nunc) & ((1u << FB) - 1u)) << (step * FB);
     }
     AVZ_STAMP(12);
     lds_barrier();
     AVZ_STAMP(2);
+  }
+
+  // ---- reference-exact decisions of the deferred frames (avz_ibm_exact.hpp)
+  if constexpr (MASK == MASK_IBM) {
+    // the unit's exact-path record (ibm_exact_units, after the block's loop): frames with a
+    // deferral, frames deferred whole, the Nyquist bin's deferrals; the per-bin deferrals
+    const uint32_t pend = pendw[0], full = pendw[1];  // block-uniform (after the last barrier)
+    KArgs& Ak = kernarg_chain_args();  // pointers not held through the loop
+    const int gxi = (Ak.max_frames + kChunk - 1) / kChunk;  // analysis_items' units
+    const int unit = slot < 0 ? b * gxi + c : gxi * Ak.batch + slot;
+    if (nyq_wave && lane == 0) {
+      reinterpret_cast<uint4*>(Ak.xpend)[unit] = make_uint4(pend, full, nyq_dfr, 0u);
+      // the block's units with deferrals, by position in its item sequence (bit 31: any
+      // past the 31st); ibm_exact_units reads only their records
+      if (pend) *reinterpret_cast<uint32_t*>(lds + G::MISC_OFF + 48) |= 1u << min(seq, 31);
+    }
+    if (DLT && pend != 0u) {
+#pragma unroll
+      for (int j = 0; j < BPT; ++j) Ak.xdfr[(long long)unit * F + tid + j * NT] = dfr[j];
+    }
   }
 
   // ---- chunk partials (a piece's: its tail slot; its bits merged into the chunk's words)
@@ -769,16 +1163,127 @@ __device__ __forceinline__ void analysis_items(const ChainArgs& A, unsigned char
                                                const LaneConst<N>& K) {
   const int P = SPLIT && A.a_pieces > 1 ? A.a_pieces : 1;
   const int n_whole = P > 1 ? A.a_whole : n_items;
-  int u = blockIdx.x;
-  for (; u < n_whole; u += gridDim.x)
-    analysis_item<N, MASK, IRM>(A, lds, u % gx, u / gx, 0, 1, -1, tw_reg, K);
-  if (SPLIT && P > 1) {
-    const int n_units = (n_items - n_whole) * P;
-    for (int q = u - n_whole; q < n_units; q += gridDim.x) {
-      const int it = n_whole + q / P;
-      analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, q % P, P, q, tw_reg, K);
+  const int n_end = n_whole + (n_items - n_whole) * P;  // whole items, then the pieces
+  // one call site (two inlined copies of the item, whole and piece, spilled)
+  int seq = 0;
+  for (int u = blockIdx.x; u < n_end; u += gridDim.x) {
+    const bool whole = u < n_whole;
+    const int q = u - n_whole, it = whole ? u : n_whole + q / P;
+    analysis_item<N, MASK, IRM>(A, lds, it % gx, it / gx, whole ? 0 : q % P, whole ? 1 : P,
+                                whole ? -1 : q, tw_reg, K, seq++);
+  }
+}
+
+// The slot of frame f of unit u (one thread): the unit's item, its length, the frame's flags.
+template <int N, bool PER_BIN, class CA>
+__device__ __forceinline__ void exact_set_slot(CA& A, XSlot* sl, int g, int u, int f, int gx,
+                                               int n_items, int n_whole, int P) {
+  constexpr int F = N / 2 + 1;
+  XSlot s;
+  s.unit = u;
+  s.f = f;
+  s.e = -1;
+  unit_item<F>(A, u, gx, n_items, n_whole, P, s.b, s.c);
+  s.L = utt_len(A, s.b);
+  const uint4 r = reinterpret_cast<const uint4*>(A.xpend)[u];
+  s.flags = (PER_BIN ? 0 : (int)((r.y >> f) & 1u)) | (int)(((r.z >> f) & 1u) << 1);
+  s.pad = 0;
+  sl[g] = s;
+}
+
+// Reference-exact decisions of analysis unit u's deferred frames (record xpend[u]: frames with
+// a deferral, frames deferred whole, the Nyquist bin's deferrals; xdfr[u][k] the per-bin
+// deferrals of the kernels without the reference-bit hand-off), rounds of up to four frames
+// in frame order (exact_round): the unit's partials of the thread's bins (kb = tid + j NT;
+// the Nyquist bin: the last thread) as running sums, + each frame's terms in frame order,
+// stored once; the noise bits OR-ed into the chunk's mask words (pieces of the chunk on other
+// blocks own the other bits). The block must have the exact phase's LDS tables (xtab_fill)
+// and the fp32 twiddle table (TW_OFF).
+template <int N, bool PER_BIN>
+__device__ __forceinline__ void exact_unit(KArgs& A, unsigned char* lds, int u, int gx, int n_items,
+                                           int n_whole, int P) {
+  using G = CGeo<N>;
+  using XL = XLds<N>;
+  constexpr int F = N / 2 + 1, NT = G::NT, BPT = G::BPT, FR = XL::FR;
+  const int tid = threadIdx.x;
+  XSlot* const sl = reinterpret_cast<XSlot*>(lds + XL::SLOT_OFF);
+  const uint32_t pend = reinterpret_cast<const uint4*>(A.xpend)[u].x;  // block-uniform
+  if (pend == 0u) return;
+  int b, c;
+  float* const Pt = unit_item<F>(A, u, gx, n_items, n_whole, P, b, c);
+  if (A.xstat && tid == 0) atomicAdd(A.xstat, (unsigned long long)__popc(pend));
+  Acc32 pacc[BPT + 1];
+  uint32_t pbits[BPT + 1];
+#pragma unroll
+  for (int j = 0; j <= BPT; ++j) {
+    const int kk = j < BPT ? tid + j * NT : N / 2;
+    pbits[j] = 0u;
+    if (j < BPT || tid == NT - 1) {
+      pacc[j].c00 = Pt[0 * F + kk];
+      pacc[j].c11 = Pt[1 * F + kk];
+      pacc[j].c01r = Pt[2 * F + kk];
+      pacc[j].c01i = Pt[3 * F + kk];
+      pacc[j].cm = Pt[4 * F + kk];
+    } else {
+      pacc[j].zero();
     }
   }
+  uint32_t rest = pend;
+  while (rest != 0u) {  // block-uniform
+    if (tid < FR) {
+      uint32_t x = rest;
+      for (int i = 0; i < tid && x; ++i) x &= x - 1u;
+      if (x) exact_set_slot<N, PER_BIN>(A, sl, tid, u, __builtin_ctz(x), gx, n_items, n_whole, P);
+    }
+    const int ns = min(FR, __popc(rest));
+    for (int i = 0; i < ns; ++i) rest &= rest - 1u;
+    __syncthreads();
+    exact_round<N, PER_BIN>(A, lds, sl, ns, pacc, pbits);
+  }
+  uint32_t* const MW = A.mwords + ((long long)b * A.nchunk + c) * F;
+#pragma unroll
+  for (int j = 0; j <= BPT; ++j) {
+    const int kk = j < BPT ? tid + j * NT : N / 2;
+    if (j < BPT || tid == NT - 1) {
+      Pt[0 * F + kk] = pacc[j].c00;
+      Pt[1 * F + kk] = pacc[j].c11;
+      Pt[2 * F + kk] = pacc[j].c01r;
+      Pt[3 * F + kk] = pacc[j].c01i;
+      Pt[4 * F + kk] = pacc[j].cm;
+      if (pbits[j]) atomicOr(MW + kk, pbits[j]);
+    }
+  }
+}
+
+// After the persistent loop: the block's units with deferrals (the unit mask, in
+// analysis_items' order), decided here (exact_unit). Blocks end their loops at different
+// times, so the exact work of one overlaps the others' loops (a separate launch spreading the
+// units over its grid ran 173 us against 159 us this way at kappa 64, configs[1]).
+template <int N, int MASK, bool IRM, bool SPLIT, class TW>
+__device__ __forceinline__ void ibm_exact_units(unsigned char* lds, int gx, int n_items) {
+  KArgs& A = kernarg_chain_args();
+  using G = CGeo<N>;
+  using XL = XLds<N>;
+  constexpr bool SHARE = N == 1024 && !std::is_same<TW, NoTw>::value;
+  constexpr bool PER_BIN = !(N == 1024 && !IRM && SHARE);  // not the reference-bit path
+  if (A.ibm_cert <= 0.0f) return;
+  const int tid = threadIdx.x;
+  const int P = SPLIT && A.a_pieces > 1 ? A.a_pieces : 1;
+  const int n_whole = P > 1 ? A.a_whole : n_items;
+  __syncthreads();  // the block's records, partials (global stores of other waves), unit mask
+  const uint32_t mine = *reinterpret_cast<const uint32_t*>(lds + G::MISC_OFF + 48);
+  if (mine == 0u) return;  // block-uniform: no deferral in any of the block's units
+  xtab_fill<N>(A.xtw, A.xwin, reinterpret_cast<cd*>(lds + XL::TWL_OFF),
+               reinterpret_cast<float*>(lds + XL::WIN_OFF), tid, G::NT);
+  __syncthreads();
+  int seq = 0;
+  auto one = [&](int u) {
+    const int k = seq++;
+    if (!((mine >> min(k, 31)) & 1u)) return;
+    exact_unit<N, PER_BIN>(A, lds, u, gx, n_items, n_whole, P);
+  };
+  const int n_end = n_whole + (n_items - n_whole) * P;  // analysis_items' sequence
+  for (int u = blockIdx.x; u < n_end; u += gridDim.x) one(u < n_whole ? u : n_items + u - n_whole);
 }
 
 // Persistent grid (about two blocks per CU): block i takes the (chunk, utterance) items
@@ -791,6 +1296,8 @@ template <int N, int MASK, bool IRM, bool SPLIT = false>
 __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysis_kernel(ChainArgs A) {
   using G = CGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
+  if (MASK == MASK_IBM && threadIdx.x == 0)  // ibm_exact_units' unit mask (after a barrier)
+    *reinterpret_cast<uint32_t*>(lds + G::MISC_OFF + 48) = 0u;
   // the per-utterance synthesis' piece finalize state, reset here (the next launch reads it)
   if (A.pstate)
     for (int b = blockIdx.x * kCThreads + threadIdx.x; b < A.batch; b += gridDim.x * kCThreads)
@@ -809,11 +1316,17 @@ __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysi
     }
     LaneConst<N> K;
     K.init(threadIdx.x);
+    if (MASK != MASK_IPD && (threadIdx.x & 32)) {  // rotated frames (pair_loads): window
+      K.wc.ac = -K.wc.ac;                          // halves swapped, once per kernel (per item
+      K.wc.as = -K.wc.as;                          // both signs stayed live and one spilled)
+    }
     analysis_items<N, MASK, IRM, SPLIT>(A, lds, gx, n_items, tw_reg, K);
+    if constexpr (MASK == MASK_IBM) ibm_exact_units<N, MASK, IRM, SPLIT, Tw1024>(lds, gx, n_items);
   } else {
     LaneConst<N> K;
     K.init(threadIdx.x);
     analysis_items<N, MASK, IRM, SPLIT>(A, lds, gx, n_items, NoTw{}, K);
+    if constexpr (MASK == MASK_IBM) ibm_exact_units<N, MASK, IRM, SPLIT, NoTw>(lds, gx, n_items);
   }
 }
 
@@ -1749,8 +2262,9 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     const long long slot0 = (long long)(b - s_whole) * pieces;
     const float iw = inv_wsum<N>(t);  // H = kUttThreads: thread t owns sample m = t
     // seam p = tail of piece p - 1 + head of piece p, 8 seams per round trip through
-    // descriptors covering the np slots (absent ones read +0); raw values to the frame
-    // slots (free at a unit's end) for the scaled write
+    // descriptors covering the np slots; raw values to the frame slots (free at a unit's end)
+    // for the scaled write. Only seams p < np enter the peak: for p = np the tail load still
+    // falls inside the descriptor (slot np - 1's tail: no seam, possibly an earlier call's)
     const rsrc_t rt = make_rsrc(A.ptails + slot0 * H, (long long)np * H);
     const rsrc_t rh = make_rsrc(A.pheads + slot0 * H, (long long)np * H);
     float* stash = reinterpret_cast<float*>(lds) + t;
@@ -1768,9 +2282,11 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        sv[u] *= iw;
-        mx = fmaxf(mx, fabsf(sv[u]));
-        if (p0 + u < np) stash[(p0 + u - 1) * H] = sv[u];
+        if (p0 + u < np) {
+          sv[u] *= iw;
+          mx = fmaxf(mx, fabsf(sv[u]));
+          stash[(p0 + u - 1) * H] = sv[u];
+        }
       }
     }
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -2123,6 +2639,14 @@ __global__ void __launch_bounds__(kUttThreads, 2) avz_synthesis_utt_kernel(Chain
     cu = unit_at((whole ? (ipf ? b + G : b)
                         : (ipf ? 0 : s_whole) + (b - s_whole) * pieces + (step - 1) / A.s_steps) +
                  gridDim.x);
+  }
+  // a piece interior still lazy: every later unit of the block was skipped (device length
+  // < N), so no whole utterance's end resolved it -- take 1/peak or hand it back now
+  // (rescale_rest's slices assume a published scale)
+  if (PIECES && ipf && rs_lazy >= 0) {
+    if (tid == 0) rs_resolve_issue();
+    __syncthreads();
+    rs_resolve();
   }
   // the block's last utterance, after the loop where the sample registers are dead: every
   // load of a 4-s utterance in flight at once (the single-utterance blocks of B <= #CU

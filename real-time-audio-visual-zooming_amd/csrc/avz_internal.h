@@ -84,9 +84,23 @@ struct ChainArgs {
   // it). Reset with peak_u by the analysis kernel.
   int s_ipf;
   PieceState* pstate;
-  int dbg_ipf;                // diagnostic (avz_debug_set_ipf_mode): 1 = every piece but the
+  int dbg_ipf;                // diagnostic (avz_plan_set_diagnostics): 1 = every piece but the
                               // last arriver hands itself back at once, 2 = pieces ignore 1/peak
                               // until their next utterance's end (the protocol's rare paths)
+  // Reference-exact IBM decisions (avz_ibm_exact.hpp): ibm_cert = kappa * 2^-24, the error
+  // bound of the fp32 reference transform per unit of frame norm (0: every decision from the
+  // fp32 transform); xwin [N] the reference's fp32 Hann window, xtw [N][2] W_N^j in fp64
+  // (plan tables); xstat (optional, [2]): deferred (bin, frame) decisions, exact noise ones.
+  float ibm_cert;
+  const float* xwin;
+  const double* xtw;
+  unsigned long long* xstat;
+  uint32_t* xpend;            // [units][4] per analysis unit (item b * gx + c, or piece
+                              // gx * B + q): frames with a deferred decision, frames deferred
+                              // whole, the Nyquist bin's deferrals (IBM plans' workspace)
+  uint32_t* xdfr;             // [units][F] per-bin deferred frames (IBM without the
+                              // reference-bit hand-off), written only for units with deferrals
+  int synth_variant;          // host-only (avz_plan_set_diagnostics): synthesis path, 2 default
   void* const* events;        // host-only: (start, stop) hipEvent_t pairs of the 4 launches, or null
   int n_events;               // host-only: how many of them to use (8, or 2: analysis only)
 };

@@ -34,7 +34,7 @@ def test_strerror_and_host_side_validation():
     lib = _lib.lib
     assert lib.avz_strerror(0) == b"ok"
     assert lib.avz_strerror(-4) == b"unsupported configuration"
-    assert lib.avz_version() == _lib.ABI_VERSION == 2
+    assert lib.avz_version() == _lib.ABI_VERSION == 3
     assert b"aligned" in lib.avz_strerror(_lib.AVZ_ERR_ALIGN)
     c = _lib.AvzConfig(fs=16000, n_fft=768, hop=384, sigma=1.0, angle_deg=90.0, mic_d=0.01,
                        c_sound=343.0, fmin_hz=100.0, mask_mode=0, postfilter=1, pf_floor=0.05,

@@ -1,4 +1,4 @@
-"""In-process A/B of the synthesis paths (avz_debug_set_synth_variant: 1 per-utterance
+"""In-process A/B of the synthesis paths (plan.set_diagnostics synth_variant: 1 per-utterance
 kernel, 0 chunk grid + finalize) on configs[1]
 (and optionally other workloads): outputs of the variants compared element-wise, then
 per-kernel HIP-event times over alternating rounds.
@@ -50,7 +50,7 @@ def main():
     variants = [int(v) for v in a.variants.split(",")]
     res = {}
     for v in variants:
-        assert lib.avz_debug_set_synth_variant(v) == 0
+        plan.set_diagnostics(synth_variant=v)
         plan.run(mix, lens, max_len=S, out=out, peak=peak, **refs)
         torch.cuda.synchronize()
         res[v] = (out.clone(), peak.clone())
@@ -69,7 +69,7 @@ def main():
     torch.cuda.synchronize()
     for r in range(a.rounds):
         for v in variants:
-            lib.avz_debug_set_synth_variant(v)
+            plan.set_diagnostics(synth_variant=v)
             for _ in range(5):
                 plan.run(mix, lens, max_len=S, out=out, peak=peak, **refs)
             plan.set_timing(True)
@@ -83,7 +83,7 @@ def main():
             plan.set_timing(False)
             print(f"round {r} variant {v}: " + " ".join(f"{k} {t[k] * 1e3:.1f}" for k in plan.KERNELS)
                   + f" us; wall {wall * 1e6:.1f} us/call (events on)", flush=True)
-    lib.avz_debug_set_synth_variant(2)  # the shipped default
+    plan.set_diagnostics(synth_variant=2)  # the shipped default
 
 
 if __name__ == "__main__":

@@ -24,11 +24,11 @@ plan = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="i
                     normalize="peak", max_batch=B, max_samples=S)
 runs = []
 for mode in (0, 0, 1, 2, 0):
-    lib.avz_debug_set_ipf_mode(mode)
+    plan.set_diagnostics(ipf_mode=mode)
     out, peak = plan.run(dm, lt, max_len=S, ref_tgt=dt, ref_int=di)
     torch.cuda.synchronize()
     runs.append((mode, out.clone().cpu().numpy(), peak.clone().cpu().numpy()))
-lib.avz_debug_set_ipf_mode(0)
+plan.set_diagnostics(ipf_mode=0)
 n_out = plan.out_len(S)
 ref = runs[1][1]
 for (mode, o, p) in runs:

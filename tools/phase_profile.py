@@ -40,14 +40,22 @@ ap.add_argument("--n-fft", type=int, default=1024)
 ap.add_argument("--mask", default="ibm")
 ap.add_argument("--normalize", default="peak")
 ap.add_argument("--seconds", type=float, default=4.0)
-ap.add_argument("--synth-variant", type=int, default=-1, help="avz_debug_set_synth_variant")
+ap.add_argument("--synth-variant", type=int, default=-1, help="plan.set_diagnostics synth_variant")
 ap.add_argument("--rows", default="",
                 help="lo:hi[,lo:hi...] block-row groups to report separately (e.g. 0:8,8:256)")
+ap.add_argument("--kappa", type=float, default=None, help="IBM plans: ibm_kappa")
+ap.add_argument("--exact", action="store_true",
+                help="label slots 4-10 as the exact IBM path's round phases (analysis)")
 ap.add_argument("--utt", action="store_true",
                 help="label slots 4-10, 13-15 as the per-utterance synthesis kernel's phases")
 a = ap.parse_args()
 if a.synth_variant >= 0 and not a.utt:
     PHASES = [RS_PHASES.get(i, n) if i >= 4 and a.synth_variant == 1 else n
+              for i, n in enumerate(PHASES)]
+if a.exact:
+    PHASES = [{4: "X loads+ref A", 5: "X ref B", 6: "X barrier 1", 7: "X mic FFT",
+               8: "X barrier 2", 9: "X bins", 10: "X barrier 3", 13: "X grid arrive",
+               14: "X scan / rounds", 15: "X grid arrive 2"}.get(i, n)
               for i, n in enumerate(PHASES)]
 if a.utt:
     PHASES = [UTT_PHASES.get(i, n) if i >= 4 and i not in (11, 12) else n
@@ -57,14 +65,16 @@ dev = torch.device("cuda:0")
 mix, tgt, itf = synth.make_batch(a.batch, n_samples=S, n_interferers=2)
 plan = avz.MVDRPlan(n_fft=a.n_fft, sigma=1.0, mic_d=0.01, mask=a.mask,
                     postfilter="ibm" if a.mask == "ibm" else "none", normalize=a.normalize,
-                    max_batch=a.batch, max_samples=S)
+                    max_batch=a.batch, max_samples=S,
+                    **({"ibm_kappa": a.kappa} if a.kappa is not None else {}))
 d = [torch.from_numpy(x).to(dev) for x in (mix, tgt, itf)]
 kw = dict(ref_tgt=d[1], ref_int=d[2]) if a.mask == "ibm" else {}
 nblk = a.batch * -(-plan.frames(S) // avz._lib.lib.avz_chunk_frames())
 st = torch.zeros((nblk, 16), dtype=torch.int64, device=dev)
 lib = avz._lib.lib
 if a.synth_variant >= 0:
-    lib.avz_debug_set_synth_variant(a.synth_variant)
+    plan.set_diagnostics(synth_variant=a.synth_variant)
+
 setter = lib.avz_debug_set_stamps_chunked
 setter.argtypes = [ct.c_void_p]
 for _ in range(3):
