@@ -33,6 +33,7 @@ struct Workspace {
   avz::PieceState* pstate;   // [batch] in-kernel piece finalize: arrivals, 1/peak, hand-backs
   uint32_t* xpend;           // IBM plans: [units][4] exact-path records (ChainArgs)
   uint32_t* xdfr;            // IBM plans: [units][F] per-bin deferrals
+  uint32_t* xunc;            // IBM plans: [units][32][32] uncertain bins of deferred frames
 };
 
 // Tail-splitting capacity (ChainArgs a_* / s_*): analysis pieces of a partial last round
@@ -65,6 +66,7 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
   const long long units = c.mask_mode == AVZ_MASK_IBM ? B * nchunk + ts : 0;
   const size_t sz_xp = align256(sizeof(uint32_t) * 4 * units);
   const size_t sz_xd = align256(sizeof(uint32_t) * (size_t)F * units);
+  const size_t sz_xu = align256(sizeof(uint32_t) * 32 * 32 * (size_t)units);
 
   if (base && w) {
     char* q = base;
@@ -85,9 +87,10 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
     w->pstate = reinterpret_cast<avz::PieceState*>(q); q += 4 * sz_b;
     w->xpend = units ? reinterpret_cast<uint32_t*>(q) : nullptr; q += sz_xp;
     w->xdfr = units ? reinterpret_cast<uint32_t*>(q) : nullptr; q += sz_xd;
+    w->xunc = units ? reinterpret_cast<uint32_t*>(q) : nullptr; q += sz_xu;
   }
   return sz_part + sz_mw + sz_coef + 2 * sz_ht + 6 * sz_b + sz_gain + sz_tpart + 2 * sz_seam +
-         sz_xp + sz_xd;
+         sz_xp + sz_xd + sz_xu;
 }
 
 struct avz_plan {
@@ -427,6 +430,7 @@ static int prepare_chain(const avz_plan* p, const avz_batch_args* a, int use, av
   k.pstate = ws.pstate;
   k.xpend = ws.xpend;
   k.xdfr = ws.xdfr;
+  k.xunc = ws.xunc;
   if (use == USE_COVARIANCE) {  // that stage produces cov_out only: leave the caller's
     k.out = nullptr;            // out / peak / w buffers untouched (the analysis kernel
     k.peak = nullptr;           // would otherwise zero peak[b] as the atomicMax target)

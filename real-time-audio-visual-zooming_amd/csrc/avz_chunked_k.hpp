@@ -232,7 +232,7 @@ __device__ __forceinline__ bool ibm_uncertain(cf zr, cf zrp, float dl) {
   return fabsf(d) < 3.9f * dl * m;
 }
 template <class After = NoAfter>
-__device__ __forceinline__ bool window_fft_reg_ibm_bits(cf (&v)[32], const WinCoef<1024>& wc,
+__device__ __forceinline__ uint32_t window_fft_reg_ibm_bits(cf (&v)[32], const WinCoef<1024>& wc,
                                                         const Fft1024x2& fft, cf* spec,
                                                         const cf (&tw_reg)[31],
                                                         const LaneMap<1024>& lm, float eg0,
@@ -275,15 +275,23 @@ __device__ __forceinline__ bool window_fft_reg_ibm_bits(cf (&v)[32], const WinCo
     }
   });
   if (AVZ_CERT_PARTS & 4) unc = slack < 0.0f;
-  const unsigned long long ub = __ballot(unc);
-  bool defer = false;
-  if (ub != 0ull) {  // rare (wave-uniform)
-    defer = ((ub >> (32 * lm.grp)) & 0xffffffffull) != 0ull;
-    if (defer) w = 0u;
+  uint32_t um = 0u;  // the lane's uncertain bins (bit k: bin l + 32 k), as its word w
+  if (__ballot(unc) != 0ull) {  // rare (wave-uniform): which bins, by the same test
+    static_for<0, 16>([&](auto kk) {
+      constexpr int k = 15 - decltype(kk)::value;
+      const int m = l + 32 * k;
+      cf zp = spec[(N - m) & (N - 1)];
+      if (k == 0 && l == 0) zp = v[0];
+      const float d = fmaf(v[k].x, zp.x, -(v[k].y * zp.y));
+      const float mm = fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)),
+                             fmaxf(fmaxf(fabsf(zp.x), fabsf(zp.y)), dl));
+      um = (um << 1) | (fmaf(-dl39, mm, fabsf(d)) < 0.0f ? 1u : 0u);
+    });
+    w &= ~um;  // their decisions are the exact path's
   }
   reinterpret_cast<uint32_t*>(spec)[l] = w;
   static_for<0, 16>([&](auto k) { after(k); });
-  return defer;
+  return um;
 }
 
 // Window + forward FFT of the synthesis kernel and of the N = 512 analysis kernel:
@@ -457,7 +465,8 @@ struct XLds {
   static constexpr int TWL_OFF = MAG_OFF + 2 * FR * MP * 4;
   static constexpr int WIN_OFF = TWL_OFF + (N / 2) * 16;    // fp32 window [N]
   static constexpr int SLOT_OFF = WIN_OFF + N * 4;           // XSlot[FR], the round's frames
-  static constexpr int SCAN_OFF = SLOT_OFF + FR * 32;       // int[256]: the deferral scan
+  static constexpr int SCAN_OFF = SLOT_OFF + FR * 32;       // int[256]: exact_sparse's items
+  static constexpr int SCAN_INTS = 256;
   static constexpr int WL = 32;                             // frames one block decides
   static constexpr int WL_OFF = SCAN_OFF + 256 * 4;         // int4[WL]: (unit, f, e, -)
   static constexpr int CTL_OFF = WL_OFF + WL * 16;          // int[8]: counts, mode
@@ -616,7 +625,9 @@ __device__ __forceinline__ void exact_round(KArgs& A, unsigned char* lds, const 
     for (int j = 0; j < BPT; ++j) {
       const int kb = tid + j * NT;
       const int kp = (N - kb) & (N - 1);
-      const bool dfr = PER_BIN ? ((A.xdfr[(long long)s.unit * F + kb] >> s.f) & 1u) : (s.flags & 1);
+      const bool dfr =
+          PER_BIN ? ((A.xdfr[(long long)s.unit * F + kb] >> s.f) & 1u)
+                  : ((A.xunc[((long long)s.unit * kChunk + s.f) * 32 + (kb & 31)] >> (kb >> 5)) & 1u);
       Acc32 a;
       a.zero();
       bool noise = false;
@@ -857,22 +868,28 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
         // block-uniform: a chunk's last step issues no loads (analysis 79.7 -> 77.0-78.3 us,
         // profiles/r04/ab_last_step_loads.txt; the other masks' kernels keep the
         // empty-descriptor loads: a second copy of their FFT spills)
-        bool whole = false;
+        uint32_t um = 0u;
         if (step + 1 < nstep) {
           if (ref)
-            whole = window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm, eg0, eg1, cert_raw, en,
-                                            load_reg);
+            um = window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm, eg0, eg1, cert_raw, en,
+                                         load_reg);
           else
             window_fft_reg(v, wc, fft, my_spec, tw_reg, lm, load_reg);
         } else {
           if (ref)
-            whole = window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm, eg0, eg1, cert_raw, en);
+            um = window_fft_reg_ibm_bits(v, wc, fft, my_spec, tw_reg, lm, eg0, eg1, cert_raw, en);
           else
             window_fft_reg(v, wc, fft, my_spec, tw_reg, lm);
         }
-        if (whole && (lane & 31) == 0) {  // rare: the frame's decisions are the exact path's
-          atomicOr(pendw, 1u << (step * FB + my_frame));
-          atomicOr(pendw + 1, 1u << (step * FB + my_frame));
+        const unsigned long long ua = __ballot(um != 0u);
+        if (ua != 0ull) {  // rare (wave-uniform): uncertain bins, the exact path's (xunc)
+          if ((ua >> (32 * lm.grp)) & 0xffffffffull) {
+            KArgs& Ak = kernarg_chain_args();
+            const int gxi = (Ak.max_frames + kChunk - 1) / kChunk;
+            const int unit = slot < 0 ? b * gxi + c : gxi * Ak.batch + slot;
+            Ak.xunc[((long long)unit * kChunk + step * FB + my_frame) * 32 + (lane & 31)] = um;
+            if ((lane & 31) == 0) atomicOr(pendw, 1u << (step * FB + my_frame));
+          }
         }
       } else {
         window_fft_reg(v, wc, fft, my_spec, tw_reg, lm, load_reg, (DLT && ref) ? &en : nullptr);
@@ -1039,10 +1056,12 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     if (nyq_wave) {
       bool noise = false, nunc = false;
       if (lane < nvalid) {
-        const cf* Zm = slot_ptr<N>(lds, lane);
+        int ln = lane;
+        opaque_i(ln);  // its slot addresses formed here (held across the items they spilled)
+        const cf* Zm = slot_ptr<N>(lds, ln);
         cf y0, y1, zr{0, 0};
         split_pair2(Zm[N / 2], Zm[N / 2], y0, y1);
-        if constexpr (MASK == MASK_IBM) zr = slot_ptr<N>(lds, FB + lane)[N / 2];
+        if constexpr (MASK == MASK_IBM) zr = slot_ptr<N>(lds, FB + ln)[N / 2];
         float wn;
         float mn = bin_mask<MASK>(A, b, y0, y1, zr, zr, N / 2, f0 + lane, noise, wn);
         if (MASK == MASK_IPD && ((ident_w >> (8 * lane)) & 1ull)) wn = mn = 0.01f;
@@ -1174,6 +1193,121 @@ __device__ __forceinline__ void analysis_items(const ChainArgs& A, unsigned char
   }
 }
 
+// Sparse form of the exact path (reference-bit path): frames with few uncertain bins decide
+// them one by one -- per item (frame f, bin k) the fp64 DFT of both references at k (rounded
+// to complex64, numpy's |.|: ref_spectrum_exact's arithmetic) and of the packed mic pair at k
+// and N - k (scaled as the analysis transform, rounded to fp32, split as the step's), one wave
+// per item over the frame's 1024 samples, reduced across the wave. items[]: LDS, f << 16 | k,
+// in frame order; the results go through LDS (res, 6 floats per item) to the bins' threads,
+// which add them to their running sums in item order.
+constexpr int kSparseMax = 12;  // uncertain bins (Nyquist included) a frame decides this way
+template <int N>
+__device__ __forceinline__ void exact_sparse(KArgs& A, unsigned char* lds, int b, int L, int c,
+                                             const int* items, int n,
+                                             Acc32 (&pacc)[CGeo<N>::BPT + 1],
+                                             uint32_t (&pbits)[CGeo<N>::BPT + 1]) {
+  using G = CGeo<N>;
+  using XL = XLds<N>;
+  constexpr int H = N / 2, NT = G::NT, BPT = G::BPT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const cd* const twl = reinterpret_cast<const cd*>(lds + XL::TWL_OFF);
+  const float* const win = reinterpret_cast<const float*>(lds + XL::WIN_OFF);
+  float* const res = reinterpret_cast<float*>(lds);  // [n][6] (the mic-spectra slots: free)
+  const rsrc_t rt = make_rsrc(A.ref_tgt + (long long)b * A.ref_stride, L);
+  const rsrc_t ri = make_rsrc(A.ref_int + (long long)b * A.ref_stride, L);
+  const float* mixb = A.mix + (long long)b * A.mix_stride;
+  const rsrc_t rm0 = make_rsrc(mixb, L), rm1 = make_rsrc(mixb + A.ch_stride, L);
+  for (int it = wave; it < n; it += NT / 64) {  // wave-uniform
+    const int item = __builtin_amdgcn_readfirstlane(items[it]);
+    const int f = item >> 16, k = item & 0xffff;
+    const int s0 = (c * kChunk + f) * H - N / 2;
+    // every sample load in flight at once (a round trip per few samples ran ~6 us per item)
+    float st[N / 64], si[N / 64], sm0[N / 64], sm1[N / 64];
+#pragma unroll
+    for (int r = 0; r < N / 64; ++r) {
+      const int m = lane + 64 * r;
+      st[r] = bload(rt, s0 + m);
+      si[r] = bload(ri, s0 + m);
+      sm0[r] = bload(rm0, s0 + m);
+      sm1[r] = bload(rm1, s0 + m);
+    }
+    double tr = 0.0, ti = 0.0, ir = 0.0, ii = 0.0, ac = 0.0, bs = 0.0, as = 0.0, bc = 0.0;
+#pragma unroll
+    for (int r = 0; r < N / 64; ++r) {
+      const int m = lane + 64 * r;
+      const double w = (double)win[m];
+      const double xt = w * (double)st[r], xi = w * (double)si[r];
+      const double a = w * (double)sm0[r], bb = w * (double)sm1[r];
+      const cd tw = xtw_at<N>(twl, (k * m) & (N - 1));  // exp(-2 pi i k m / N)
+      tr = fma(xt, tw.x, tr);
+      ti = fma(xt, tw.y, ti);
+      ir = fma(xi, tw.x, ir);
+      ii = fma(xi, tw.y, ii);
+      ac = fma(a, tw.x, ac);
+      bs = fma(bb, tw.y, bs);
+      as = fma(a, tw.y, as);
+      bc = fma(bb, tw.x, bc);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      tr += __shfl_xor(tr, o, 64);
+      ti += __shfl_xor(ti, o, 64);
+      ir += __shfl_xor(ir, o, 64);
+      ii += __shfl_xor(ii, o, 64);
+      ac += __shfl_xor(ac, o, 64);
+      bs += __shfl_xor(bs, o, 64);
+      as += __shfl_xor(as, o, 64);
+      bc += __shfl_xor(bc, o, 64);
+    }
+    if (lane == 0) {
+      const bool noise = np_abs_c64((float)ir, (float)ii) > np_abs_c64((float)tr, (float)ti);
+      constexpr double sc = 2.0 / N;  // the analysis transform's scale ((2/N) Hann window)
+      const cf zk = {(float)(sc * (ac - bs)), (float)(sc * (as + bc))};   // Z[k]
+      const cf zp = {(float)(sc * (ac + bs)), (float)(sc * (bc - as))};   // Z[N - k]
+      Acc32 t;
+      t.zero();
+      cf x0, x1;
+      split_pair2(zk, zp, x0, x1);
+      if (k == N / 2) {
+        const float wn = noise ? 1.0f : 0.0f;
+        t.add(x0, x1, wn, wn);
+      } else {
+        t.add_sel(x0, x1, noise);
+        t.cm = noise ? 1.0f : 0.0f;
+      }
+      float* q = res + 6 * it;
+      q[0] = noise ? 1.0f : 0.0f;
+      q[1] = t.c00;
+      q[2] = t.c11;
+      q[3] = t.c01r;
+      q[4] = t.c01i;
+      q[5] = t.cm;
+    }
+  }
+  __syncthreads();
+  for (int it = 0; it < n; ++it) {  // block-uniform, item (frame) order
+    const int item = items[it];
+    const int f = item >> 16, k = item & 0xffff;
+    const int j = k == N / 2 ? BPT : k / NT;
+    if (k == N / 2 ? tid == NT - 1 : (k % NT) == tid) {
+      const float* q = res + 6 * it;
+#pragma unroll
+      for (int jj = 0; jj <= BPT; ++jj) {  // a constant index (indexed, the array went to scratch)
+        if (jj != j) continue;
+        pacc[jj].c00 += q[1];
+        pacc[jj].c11 += q[2];
+        pacc[jj].c01r += q[3];
+        pacc[jj].c01i += q[4];
+        pacc[jj].cm += q[5];
+        pbits[jj] |= (q[0] != 0.0f ? 1u : 0u) << f;
+      }
+    }
+  }
+  if (A.xstat && tid == 0) atomicAdd(A.xstat + 1, (unsigned long long)n);  // diagnostic
+  __syncthreads();
+}
+
 // The slot of frame f of unit u (one thread): the unit's item, its length, the frame's flags.
 template <int N, bool PER_BIN, class CA>
 __device__ __forceinline__ void exact_set_slot(CA& A, XSlot* sl, int g, int u, int f, int gx,
@@ -1229,6 +1363,51 @@ __device__ __forceinline__ void exact_unit(KArgs& A, unsigned char* lds, int u, 
     }
   }
   uint32_t rest = pend;
+  if constexpr (!PER_BIN) {
+    // frames with at most kSparseMax uncertain bins (the Nyquist bin included): their items in
+    // frame order (wave 0, one frame at a time), decided one by one (exact_sparse)
+    int* const items = reinterpret_cast<int*>(lds + XL::SCAN_OFF);  // [32 kSparseMax / 2]
+    int* const ctl = reinterpret_cast<int*>(lds + XL::CTL_OFF);
+    // the pending frames' words in LDS first (one round trip; per frame it was one each)
+    uint32_t* const wsm = reinterpret_cast<uint32_t*>(lds + 16384);  // [32][32] (slots: free)
+#pragma unroll
+    for (int i = 0; i < kChunk / (G::NT / 32); ++i) {
+      const int f = (tid >> 5) + (G::NT / 32) * i;
+      if ((pend >> f) & 1u) wsm[f * 32 + (tid & 31)] = A.xunc[((long long)u * kChunk + f) * 32 + (tid & 31)];
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const uint32_t nyq = reinterpret_cast<const uint4*>(A.xpend)[u].z;
+      int base = 0;
+      uint32_t sparse = 0u;
+      for (uint32_t todo = pend; todo != 0u; todo &= todo - 1u) {  // wave-uniform
+        const int f = __builtin_ctz(todo);
+        const uint32_t w = tid < 32 ? wsm[f * 32 + tid] : 0u;
+        int inc = __popc(w);
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          const int y = __shfl_up(inc, o, 64);
+          if ((tid & 63) >= o) inc += y;
+        }
+        const int tot = __shfl(inc, 31, 64), ny = (nyq >> f) & 1u;
+        if (tot + ny <= kSparseMax && base + tot + ny <= XL::SCAN_INTS) {
+          int at = base + inc - __popc(w);
+          for (uint32_t x = w; x != 0u; x &= x - 1u) items[at++] = (f << 16) | (tid + 32 * __builtin_ctz(x));
+          if (ny && tid == 0) items[base + tot] = (f << 16) | (N / 2);
+          base += tot + ny;
+          sparse |= 1u << f;
+        }
+      }
+      if (tid == 0) {
+        ctl[0] = base;
+        ctl[1] = (int)sparse;
+      }
+    }
+    __syncthreads();
+    const int n_sp = ctl[0];
+    rest &= ~(uint32_t)ctl[1];
+    if (n_sp > 0) exact_sparse<N>(A, lds, b, utt_len(A, b), c, items, n_sp, pacc, pbits);
+  }
   while (rest != 0u) {  // block-uniform
     if (tid < FR) {
       uint32_t x = rest;

@@ -100,6 +100,8 @@ struct ChainArgs {
                               // whole, the Nyquist bin's deferrals (IBM plans' workspace)
   uint32_t* xdfr;             // [units][F] per-bin deferred frames (IBM without the
                               // reference-bit hand-off), written only for units with deferrals
+  uint32_t* xunc;             // [units][32 frames][32] reference-bit path: the frame's
+                              // uncertain bins (word l bit k: bin l + 32 k), deferred frames only
   int synth_variant;          // host-only (avz_plan_set_diagnostics): synthesis path, 2 default
   void* const* events;        // host-only: (start, stop) hipEvent_t pairs of the 4 launches, or null
   int n_events;               // host-only: how many of them to use (8, or 2: analysis only)
