@@ -633,8 +633,30 @@ def run_timed(step, plan, K, W, world, dev, settle_on, kernel_timing):
     return t1 - t0, kt, settle
 
 
+def sq_busy(kernel_prefix, n_cu, batch):
+    """VALU / LDS busy fractions of a kernel from profiles/pmc_sq.json (tools/pmc_sq.sh on this
+    configuration, B = batch), or {} when there is none."""
+    path = os.path.join(ROOT, "profiles", "pmc_sq.json")
+    if not os.path.exists(path):
+        return {}
+    doc = json.load(open(path))
+    if doc.get("batch") != batch:
+        return {}
+    for k, c in doc.get("kernels", {}).items():
+        if k.startswith(kernel_prefix) and c.get("GRBM_GUI_ACTIVE"):
+            cyc = c["GRBM_GUI_ACTIVE"] / 8.0
+            r = {"sq_source": doc.get("source"), "sq_kernel": k}
+            if "SQ_ACTIVE_INST_VALU" in c:
+                r["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4.0 / (4.0 * n_cu) / cyc
+            if "SQ_LDS_IDX_ACTIVE" in c:
+                r["lds_busy"] = c["SQ_LDS_IDX_ACTIVE"] / n_cu / cyc
+            return r
+    return {}
+
+
 def secondary_entry(spec, info, K, elapsed, kt, world):
-    """A secondary configuration's figures, measured as the headline's."""
+    """A secondary configuration's figures, measured as the headline's; its dominant kernel
+    is the longest of the untimed all-kernel pass, as the headline's."""
     value = world * info["bins"] * K / elapsed
     bpb = bytes_per_bin(spec["workload"], spec["n_fft"])
     e = {"config": spec["text"], "value": value, "unit": "TF-bins/s",
@@ -642,10 +664,19 @@ def secondary_entry(spec, info, K, elapsed, kt, world):
          "frac": value / world * bpb / 1e9 / HBM_PEAK_GBS, "bytes_per_bin": bpb,
          "tf_bins_per_step": info["bins"]}
     if kt:
-        e["kernels_ms"] = {k: kt[k] for k in info["plan"].KERNELS}
-        dom_ms = kt["analysis_timed"]
-        e["dominant_kernel"] = {"kernel": info["kernel"], "kernel_ms": dom_ms,
-                                "frac": info["alg_analysis"] / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        plan = info["plan"]
+        e["kernels_ms"] = {k: kt[k] for k in plan.KERNELS}
+        name = max(plan.KERNELS, key=lambda k: kt[k] if kt[k] == kt[k] else -1.0)
+        if name == "analysis":
+            dom_ms = kt["analysis_timed"]
+            e["dominant_kernel"] = {"kernel": info["kernel"], "role": name, "kernel_ms": dom_ms,
+                                    "frac": info["alg_analysis"] / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        else:
+            ms = kt[name]
+            alg = info["alg_kernel"].get(name, 0)
+            e["dominant_kernel"] = {"kernel": info["kernel_names"].get(name, name), "role": name,
+                                    "kernel_ms": ms,
+                                    "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     return e
 
 
@@ -834,6 +865,8 @@ def main():
                "achieved": alg_analysis / (dom_ms * 1e-3) / 1e9,
                "frac": alg_analysis / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                "traffic": traffic.get("analysis")}
+        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+        ana.update(sq_busy("avz_analysis_kernel", n_cu, B))
         roof["analysis_kernel"] = ana
         # the kernel that bounds the step: the longest of the untimed pass
         name = max(plan.KERNELS, key=lambda k: kt[k] if kt[k] == kt[k] else -1.0)
@@ -851,6 +884,7 @@ def main():
                 "design_bytes_per_launch": design,
                 "frac_design": design / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "traffic": traffic.get(name),
+                **sq_busy(info["kernel_names"].get(name, name).split("<")[0], n_cu, B),
                 "note": ("alg: its compulsory bytes (the output stream); design: + the mixture "
                          "re-read of the recompute design (the forward FFT is recomputed "
                          "instead of storing Y), the IBM words and the covariance partials; "

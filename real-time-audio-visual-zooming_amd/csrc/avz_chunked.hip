@@ -1,19 +1,23 @@
-// avz_chunked.hip — launchers of the chunk-parallel chain (kernels: avz_chunked_k.hpp; the
-// analysis and synthesis instantiations are compiled in their own units, avz_chunked_inst.hpp).
+// avz_chunked.hip — launchers of the chunk-parallel chain and the per-utterance synthesis
+// kernels (kernels: avz_chunked_k.hpp; the analysis and chunk-synthesis instantiations are
+// compiled in their own units, avz_chunked_inst.hpp).
 #include "avz_chunked_k.hpp"
 #include "avz_chunked_inst.hpp"
 
 namespace avz {
-#ifdef AVZ_ONE_TU  // diagnostic: every kernel compiled in this unit (the pre-split build)
+#ifdef AVZ_ONE_TU  // the shipped build: every chain kernel compiled in this unit (Makefile)
 #define AVZ_INST template
 #else
 #define AVZ_INST extern template
 #endif
 AVZ_ANALYSIS_INST(1024)
 AVZ_ANALYSIS_INST(512)
-AVZ_UTT_INST
 AVZ_SYN_INST(1024)
 AVZ_SYN_INST(512)
+#undef AVZ_INST
+// the per-utterance synthesis kernels: with the launchers in either build
+#define AVZ_INST template
+AVZ_UTT_INST
 #undef AVZ_INST
 }  // namespace avz
 
@@ -180,14 +184,17 @@ static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, h
 }
 
 #ifdef AVZ_STAMPS
+#ifndef AVZ_ONE_TU
 extern "C" int avz_stamps_set_ana1024(void*);
 extern "C" int avz_stamps_set_ana512(void*);
-extern "C" int avz_stamps_set_utt(void*);
 extern "C" int avz_stamps_set_syn(void*);
+#endif
 extern "C" int avz_debug_set_stamps_chunked(void* dev_ptr) {
   int r = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -3;
-  r |= avz_stamps_set_ana1024(dev_ptr) | avz_stamps_set_ana512(dev_ptr);
-  return r | avz_stamps_set_utt(dev_ptr) | avz_stamps_set_syn(dev_ptr);
+#ifndef AVZ_ONE_TU
+  r |= avz_stamps_set_ana1024(dev_ptr) | avz_stamps_set_ana512(dev_ptr) | avz_stamps_set_syn(dev_ptr);
+#endif
+  return r;
 }
 #endif
 

@@ -1,5 +1,5 @@
 // avz_chunked_inst.hpp — the chain kernels' instantiations, one list for both sides: the
-// kernel translation units (avz_chunked_{ana1024,ana512,utt,syn}.hip) define them
+// kernel translation units (avz_chunked_{ana1024,ana512,syn}.hip) define them
 // (AVZ_INST = template), avz_chunked.hip declares them (AVZ_INST = extern template) so its
 // launchers reference the other units' kernels instead of compiling them again. Split only to
 // compile the device code in parallel; one list keeps the two sides in step.

@@ -34,3 +34,5 @@ for k, c in agg.items():
     for x in sorted(c):
         print(f"   {x:24s} {c[x] / len(disp[(k, x)]):16.0f}")
 PY
+# per-dispatch averages -> profiles/pmc_sq.json (bench.py's valu_busy / lds_busy)
+python3 tools/pmc_sq_json.py $out "$@" || exit 1
