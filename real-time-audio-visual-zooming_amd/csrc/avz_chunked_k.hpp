@@ -625,9 +625,13 @@ __device__ __forceinline__ void exact_round(KArgs& A, unsigned char* lds, const 
     for (int j = 0; j < BPT; ++j) {
       const int kb = tid + j * NT;
       const int kp = (N - kb) & (N - 1);
+      // the reference-bit path: the frame's xunc words (written this launch only for frames
+      // flagged by the reference waves, flags bit 0; a frame deferred for its Nyquist bin
+      // alone has none)
       const bool dfr =
           PER_BIN ? ((A.xdfr[(long long)s.unit * F + kb] >> s.f) & 1u)
-                  : ((A.xunc[((long long)s.unit * kChunk + s.f) * 32 + (kb & 31)] >> (kb >> 5)) & 1u);
+                  : ((s.flags & 1) &&
+                     ((A.xunc[((long long)s.unit * kChunk + s.f) * 32 + (kb & 31)] >> (kb >> 5)) & 1u));
       Acc32 a;
       a.zero();
       bool noise = false;
@@ -715,7 +719,7 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     int z = 0;
     opaque_i(z);  // formed here (a zero pair held across the items spilled)
     pendw[0] = (uint32_t)z;  // frames with a deferred decision
-    pendw[1] = (uint32_t)z;  // frames deferred whole (reference-bit path)
+    pendw[1] = (uint32_t)z;  // frames with uncertain bins in xunc (reference-bit path)
   }
 
   const typename C::Fft fft = K.fft;
@@ -888,7 +892,10 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
             const int gxi = (Ak.max_frames + kChunk - 1) / kChunk;
             const int unit = slot < 0 ? b * gxi + c : gxi * Ak.batch + slot;
             Ak.xunc[((long long)unit * kChunk + step * FB + my_frame) * 32 + (lane & 31)] = um;
-            if ((lane & 31) == 0) atomicOr(pendw, 1u << (step * FB + my_frame));
+            if ((lane & 31) == 0) {  // a frame with a deferral, one with its xunc words written
+              atomicOr(pendw, 1u << (step * FB + my_frame));
+              atomicOr(pendw + 1, 1u << (step * FB + my_frame));
+            }
           }
         }
       } else {
@@ -1095,7 +1102,8 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   // ---- reference-exact decisions of the deferred frames (avz_ibm_exact.hpp)
   if constexpr (MASK == MASK_IBM) {
     // the unit's exact-path record (ibm_exact_units, after the block's loop): frames with a
-    // deferral, frames deferred whole, the Nyquist bin's deferrals; the per-bin deferrals
+    // deferral, frames with xunc words (reference-bit path), the Nyquist bin's deferrals; the
+    // per-bin deferrals
     const uint32_t pend = pendw[0], full = pendw[1];  // block-uniform (after the last barrier)
     KArgs& Ak = kernarg_chain_args();  // pointers not held through the loop
     const int gxi = (Ak.max_frames + kChunk - 1) / kChunk;  // analysis_items' units
@@ -1326,7 +1334,8 @@ __device__ __forceinline__ void exact_set_slot(CA& A, XSlot* sl, int g, int u, i
 }
 
 // Reference-exact decisions of analysis unit u's deferred frames (record xpend[u]: frames with
-// a deferral, frames deferred whole, the Nyquist bin's deferrals; xdfr[u][k] the per-bin
+// a deferral, frames with uncertain-bin words xunc[u][f] (reference-bit path), the Nyquist
+// bin's deferrals; xdfr[u][k] the per-bin
 // deferrals of the kernels without the reference-bit hand-off), rounds of up to four frames
 // in frame order (exact_round): the unit's partials of the thread's bins (kb = tid + j NT;
 // the Nyquist bin: the last thread) as running sums, + each frame's terms in frame order,
@@ -1370,10 +1379,13 @@ __device__ __forceinline__ void exact_unit(KArgs& A, unsigned char* lds, int u, 
     int* const ctl = reinterpret_cast<int*>(lds + XL::CTL_OFF);
     // the pending frames' words in LDS first (one round trip; per frame it was one each)
     uint32_t* const wsm = reinterpret_cast<uint32_t*>(lds + 16384);  // [32][32] (slots: free)
+    const uint32_t has_words = reinterpret_cast<const uint4*>(A.xpend)[u].y;  // see exact_round
 #pragma unroll
     for (int i = 0; i < kChunk / (G::NT / 32); ++i) {
       const int f = (tid >> 5) + (G::NT / 32) * i;
-      if ((pend >> f) & 1u) wsm[f * 32 + (tid & 31)] = A.xunc[((long long)u * kChunk + f) * 32 + (tid & 31)];
+      if ((pend >> f) & 1u)
+        wsm[f * 32 + (tid & 31)] =
+            ((has_words >> f) & 1u) ? A.xunc[((long long)u * kChunk + f) * 32 + (tid & 31)] : 0u;
     }
     __syncthreads();
     if (tid < 64) {

@@ -152,3 +152,28 @@ def test_exact_path_is_deterministic(avz, gpu_device, kappa):
         assert torch.equal(x, y)
     print(f"kappa {kappa:g}: {int(res[0][3][0])} frames, {int(res[0][3][1])} decisions on the "
           "exact path; two calls bitwise equal")
+
+
+def test_exact_path_ignores_an_earlier_calls_words(avz, gpu_device):
+    """The uncertain-bin words (xunc) are written only for the frames a call flags; a frame
+    deferred for its Nyquist bin alone has none, and must not read an earlier call's. One plan
+    runs batch A (utterances 4242..) and then batch B (0..): B's outputs, peaks and covariances
+    equal a fresh plan's bitwise."""
+    from avz import synth
+    S, B = 64000, 64
+    kw = dict(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm", normalize="peak",
+              max_batch=B, max_samples=S)
+    a = synth.make_batch_device(B, start=4242, n_samples=S, n_interferers=2, device=gpu_device,
+                                rng="philox")
+    dm, dt, di = synth.make_batch_device(B, start=0, n_samples=S, n_interferers=2,
+                                         device=gpu_device, rng="philox")
+    used = avz.MVDRPlan(**kw)
+    used.run(a[0], ref_tgt=a[1], ref_int=a[2])
+    res = []
+    for plan in (used, avz.MVDRPlan(**kw)):
+        cov = torch.zeros((B, 513, 5), dtype=torch.float64, device=gpu_device)
+        out, peak = plan.run(dm, ref_tgt=dt, ref_int=di, cov_out=cov)
+        torch.cuda.synchronize()
+        res.append((out.clone(), peak.clone(), cov))
+    for x, y in zip(res[0], res[1]):
+        assert torch.equal(torch.nan_to_num(x, nan=7.0), torch.nan_to_num(y, nan=7.0))

@@ -1,6 +1,6 @@
 set -o pipefail
-mkdir -p gpurun_out/r06v
-timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_parity.py -k "seams or skipped or multi_round" > gpurun_out/r06v/pytest.log 2>&1; rc=$?
-grep -E "PASS|FAIL|Error|assert" gpurun_out/r06v/pytest.log | head -20
-[ $rc -eq 0 ] || exit 1
-bash tools/gpu_ab_r06.sh r06v 2 "base|AVZ_LIB=ab/base/libavz.so python bench.py --ibm-kappa -1" "pk|AVZ_LIB=ab/pk/libavz.so python bench.py --ibm-kappa -1" "basek|AVZ_LIB=ab/base/libavz.so python bench.py" "pkk|AVZ_LIB=ab/pk/libavz.so python bench.py" "old|cd ab/r05 && python bench.py"
+mkdir -p gpurun_out/r06z
+timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/r06z/pytest.log 2>&1; echo "full rc $?"
+tail -5 gpurun_out/r06z/pytest.log
+timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_hybrid.py tests/test_gpu_ibm_exact.py > gpurun_out/r06z/pytest2.log 2>&1; echo "again rc $?"
+tail -3 gpurun_out/r06z/pytest2.log
