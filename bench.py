@@ -673,9 +673,9 @@ def secondary_entry(spec, info, K, elapsed, kt, world):
                                     "frac": info["alg_analysis"] / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
         else:
             ms = kt[name]
-            alg = info["alg_kernel"].get(name, 0)
-            e["dominant_kernel"] = {"kernel": info["kernel_names"].get(name, name), "role": name,
-                                    "kernel_ms": ms,
+            alg = info.get("alg_kernel", {}).get(name, 0)
+            e["dominant_kernel"] = {"kernel": info.get("kernel_names", {}).get(name, name),
+                                    "role": name, "kernel_ms": ms,
                                     "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     return e
 

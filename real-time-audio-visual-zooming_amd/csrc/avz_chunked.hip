@@ -376,7 +376,9 @@ static int launch_cov_t(const ChainArgs* a, hipStream_t st) {
   const int n_items = nch * a->batch;
   ChainArgs c = *a;
   c.cov_only = 1;
-  // the chain's tail splitting, so the sums equal the fused call's bitwise
+  // the chain's tail splitting, so the sums equal the fused call's bitwise (but where the
+  // solve lanes kernel sums a small split batch: its fp64 association differs, equal up to
+  // fp64 rounding)
   constexpr int SA = kChunk / ((MASK == MASK_IBM) ? CGeo<N>::NSLOT / 2 : CGeo<N>::NSLOT);
   const int grid = analysis_tail(c, n_items, CGeo<N>::BLOCKS * resident_cus(), SA);
   const bool split = c.a_pieces > 1;

@@ -391,7 +391,10 @@ def test_split_batch_unfused_solve_bitwise(avz, gpu_device, B):
     """A split batch with the covariance / weight debug outputs takes the solve kernel and
     the per-utterance kernel's copying instance (pieces included: B = 1 below the CU count,
     B = 257 through the in-kernel piece finalize); its outputs and peaks equal the fused
-    in-block solve's bitwise, and the debug covariances are finite for every valid bin."""
+    in-block solve's -- bitwise at B = 257 (the solve kernel sums each bin's partials in the
+    fused solve's order), within 1e-6 at B = 1, whose few bins take the solve lanes kernel
+    (fp64 partial sums over 8 lanes combined by a tree: another association) --
+    and the debug covariances are finite for every valid bin."""
     from avz import synth
     S = 64000
     dm, dt, di = synth.make_batch_device(B, start=901, n_samples=S, n_interferers=2,
@@ -405,8 +408,12 @@ def test_split_batch_unfused_solve_bitwise(avz, gpu_device, B):
     out_d, peak_d = plan.run(dm, ref_tgt=dt, ref_int=di, cov_out=cov, w_out=w)
     torch.cuda.synchronize()
     n = plan.out_len(S)
-    assert torch.equal(out[:, :n], out_d[:, :n])
-    assert torch.equal(peak, peak_d)
+    if B > 1:
+        assert torch.equal(out[:, :n], out_d[:, :n])
+        assert torch.equal(peak, peak_d)
+    else:
+        torch.testing.assert_close(out_d[:, :n], out[:, :n], rtol=0, atol=1e-6)
+        torch.testing.assert_close(peak_d, peak, rtol=1e-6, atol=0)
     assert bool(torch.isfinite(cov).all())
 
 
