@@ -34,6 +34,10 @@ struct Workspace {
   uint32_t* xpend;           // IBM plans: [units][4] exact-path records (ChainArgs)
   uint32_t* xdfr;            // IBM plans: [units][F] per-bin deferrals
   uint32_t* xunc;            // IBM plans: [units][32][32] uncertain bins of deferred frames
+  uint32_t* xst;             // IBM plans: [units][2] work-sharing state (must start zero)
+  size_t xst_bytes;
+  long long xst_units;
+  float* xres;               // IBM plans: [units][kXPieces][5][F] shared units' piece sums
 };
 
 // Tail-splitting capacity (ChainArgs a_* / s_*): analysis pieces of a partial last round
@@ -67,6 +71,8 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
   const size_t sz_xp = align256(sizeof(uint32_t) * 4 * units);
   const size_t sz_xd = align256(sizeof(uint32_t) * (size_t)F * units);
   const size_t sz_xu = align256(sizeof(uint32_t) * 32 * 32 * (size_t)units);
+  const size_t sz_xs = align256(sizeof(uint32_t) * (2 * (size_t)units + (size_t)(units + 31) / 32));
+  const size_t sz_xr = align256(sizeof(float) * avz::kXPieces * 5 * (size_t)F * units);
 
   if (base && w) {
     char* q = base;
@@ -88,9 +94,13 @@ static size_t ws_layout(const avz_config& c, long long batch, int nchunk, char* 
     w->xpend = units ? reinterpret_cast<uint32_t*>(q) : nullptr; q += sz_xp;
     w->xdfr = units ? reinterpret_cast<uint32_t*>(q) : nullptr; q += sz_xd;
     w->xunc = units ? reinterpret_cast<uint32_t*>(q) : nullptr; q += sz_xu;
+    w->xst = units ? reinterpret_cast<uint32_t*>(q) : nullptr; q += sz_xs;
+    w->xst_bytes = sz_xs;
+    w->xst_units = units;
+    w->xres = units ? reinterpret_cast<float*>(q) : nullptr; q += sz_xr;
   }
   return sz_part + sz_mw + sz_coef + 2 * sz_ht + 6 * sz_b + sz_gain + sz_tpart + 2 * sz_seam +
-         sz_xp + sz_xd + sz_xu;
+         sz_xp + sz_xd + sz_xu + sz_xs + sz_xr;
 }
 
 struct avz_plan {
@@ -246,6 +256,14 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
     p->xtw = reinterpret_cast<double*>(q + sz_steer);
     p->xwin = reinterpret_cast<float*>(q + sz_steer + sz_xtw);
     ws_layout(c, c.max_batch, p->nchunk, q + sz_tab, &p->ws);
+    if (p->ws.xst) {  // the exact path's work-sharing state starts zero (launches leave it so)
+      e = hipMemset(p->ws.xst, 0, p->ws.xst_bytes);
+      if (e != hipSuccess) {
+        (void)hipFree(p->arena);
+        delete p;
+        return hip_fail(e);
+      }
+    }
     const double kappa = c.ibm_kappa == 0.0 ? AVZ_IBM_KAPPA : c.ibm_kappa;
     p->ibm_cert = kappa > 0.0 ? (float)(kappa * 0x1p-24) : 0.0f;
     p->xstat = nullptr;
@@ -393,6 +411,7 @@ static int prepare_chain(const avz_plan* p, const avz_batch_args* a, int use, av
     ws_layout(c, a->batch, nchunk, static_cast<char*>(a->workspace), &ws);
   }
   k = avz::ChainArgs{};
+  k.xst_reset = (a->workspace && ws.xst) ? (long long)ws.xst_bytes : 0;
   plan_params(p, k);
   k.batch = a->batch;
   k.len = a->len;
@@ -431,6 +450,9 @@ static int prepare_chain(const avz_plan* p, const avz_batch_args* a, int use, av
   k.xpend = ws.xpend;
   k.xdfr = ws.xdfr;
   k.xunc = ws.xunc;
+  k.xst = ws.xst;
+  k.xres = ws.xres;
+  k.xhint = ws.xst ? ws.xst + 2 * (ws.xst_units) : nullptr;
   if (use == USE_COVARIANCE) {  // that stage produces cov_out only: leave the caller's
     k.out = nullptr;            // out / peak / w buffers untouched (the analysis kernel
     k.peak = nullptr;           // would otherwise zero peak[b] as the atomicMax target)
@@ -460,6 +482,8 @@ extern "C" int avz_mvdr_batch(const avz_plan* p, const avz_batch_args* a, void* 
     k.events = evs;
     k.n_events = 2 * mp->n_k;
   }
+  if (k.xst_reset && hipMemsetAsync(k.xst, 0, (size_t)k.xst_reset, (hipStream_t)stream) != hipSuccess)
+    return hip_rc(AVZ_ERR_HIP);
   const int rc = hip_rc(avz_launch_chunked(p->cfg.n_fft, p->cfg.mask_mode, &k, stream));
   if (set >= 0 && rc == AVZ_OK) {
     mp->ev_pending[set] = true;
@@ -473,6 +497,8 @@ extern "C" int avz_mvdr_covariance(const avz_plan* p, const avz_batch_args* a, v
   avz::ChainArgs k;
   const int e = prepare_chain(p, a, USE_COVARIANCE, k);
   if (e != AVZ_OK) return e;
+  if (k.xst_reset && hipMemsetAsync(k.xst, 0, (size_t)k.xst_reset, (hipStream_t)stream) != hipSuccess)
+    return hip_rc(AVZ_ERR_HIP);
   return hip_rc(avz_launch_covariance(p->cfg.n_fft, p->cfg.mask_mode, &k, stream));
 }
 

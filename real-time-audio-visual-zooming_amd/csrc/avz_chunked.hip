@@ -183,7 +183,7 @@ static int launch_synthesis(const ChainArgs* a, hipStream_t st, hipEvent_t e0, h
   return 0;
 }
 
-#ifdef AVZ_STAMPS
+#if defined(AVZ_STAMPS) || defined(AVZ_XTRACE)
 #ifndef AVZ_ONE_TU
 extern "C" int avz_stamps_set_ana1024(void*);
 extern "C" int avz_stamps_set_ana512(void*);

@@ -9,7 +9,7 @@ AVZ_ANALYSIS_INST(1024)
 #undef AVZ_INST
 }  // namespace avz
 
-#ifdef AVZ_STAMPS
+#if defined(AVZ_STAMPS) || defined(AVZ_XTRACE)
 extern "C" int avz_stamps_set_ana1024(void* p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(avz::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -3;
 }

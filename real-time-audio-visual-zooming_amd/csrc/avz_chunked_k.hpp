@@ -536,6 +536,19 @@ __device__ __forceinline__ void exact_round(KArgs& A, unsigned char* lds, const 
   cd* const buf = reinterpret_cast<cd*>(lds + wave * X::SCRATCH);
   AVZ_STAMP_DECL();
   AVZ_STAMP_INIT();
+#ifdef AVZ_XTRACE  // diagnostic: phase ticks of the rounds (tools/xtrace.py)
+  unsigned long long xr_prev = __builtin_amdgcn_s_memrealtime();
+#define AVZ_XR(i)                                                                  \
+  do {                                                                             \
+    if (threadIdx.x == 0 && g_stamps) {                                            \
+      const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();            \
+      g_stamps[blockIdx.x * 16 + (i)] += now_ - xr_prev;                           \
+      xr_prev = now_;                                                              \
+    }                                                                              \
+  } while (0)
+#else
+#define AVZ_XR(i) (void)0
+#endif
   // lane-derived addresses formed here (hoisted out of the caller's loop they spilled)
   int lane_o = lane;
   opaque_i(lane_o);
@@ -555,6 +568,7 @@ __device__ __forceinline__ void exact_round(KArgs& A, unsigned char* lds, const 
   }
   if (ga < ns) ref_spectrum_exact<N>(xa, twl, win, buf, mag + (2 * ga + (wave & 1)) * MP, lane_o);
   AVZ_STAMP(4);
+  AVZ_XR(8);
   // waves 0-1: the mic frames' loads (one slot per lane group), in flight through the second
   // transform
   cf v[PPL];
@@ -584,6 +598,7 @@ __device__ __forceinline__ void exact_round(KArgs& A, unsigned char* lds, const 
   AVZ_STAMP(5);
   lds_barrier();  // the transform buffers are the mic spectra's slots
   AVZ_STAMP(6);
+  AVZ_XR(9);
   if (wave < XL::FR / C::FPW) {  // the mic spectra (zeros for an absent slot)
     WinCoef<N> wc;
     wc.init(lm);
@@ -605,6 +620,7 @@ __device__ __forceinline__ void exact_round(KArgs& A, unsigned char* lds, const 
   AVZ_STAMP(7);
   lds_barrier();
   AVZ_STAMP(8);
+  AVZ_XR(10);
   // decisions |I| > |T| and the frames' covariance terms, thread per bin as the step's,
   // onto the caller's running sums (one unit's frames, in frame order)
   unsigned long long n_exact = 0;
@@ -665,8 +681,41 @@ __device__ __forceinline__ void exact_round(KArgs& A, unsigned char* lds, const 
   AVZ_STAMP(9);
   lds_barrier();
   AVZ_STAMP(10);
+  AVZ_XR(11);
+#undef AVZ_XR
 }
 
+
+// A deferred frame with at most kSparseMax uncertain bins (the Nyquist bin included) is decided
+// bin by bin (exact_sparse); the reference-bit path's analysis items mark frames with
+// kSparseMax or more uncertain bins as "round" frames (fp64 transforms, exact_round) and
+// publish a unit with any for the whole grid to share (ibm_exact_units).
+constexpr int kSparseMax = 12;
+
+// Work sharing of the exact path (reference-bit path). A published unit's pieces: its sparse
+// frames (if any), then its rounds of kXRound round frames in up to kXPieces - 1 groups (two
+// frames a round: one fp64 transform per wave, the round's latency about halved against four).
+// xst[u] = {state, arrivals}: state kXOpen | pieces << 16 | next piece while open; claims add
+// 1 (a claim past the last piece, or after the reset, finds no piece: harmless); the piece that
+// completes a unit resets it to 0. xhint: one bit per published unit, cleared with the reset.
+constexpr uint32_t kXOpen = 0x80000000u;
+constexpr int kXRound = 2;
+struct XPieces {
+  uint32_t sp;           // sparse frames
+  int n_sp, nr, npr, n;  // sparse pieces (0 / 1), rounds, round pieces, pieces
+};
+__device__ __forceinline__ XPieces x_pieces(uint32_t pend, uint32_t big) {
+  XPieces q;
+  q.sp = pend & ~big;
+  q.n_sp = q.sp ? 1 : 0;
+  q.nr = (__popc(big) + kXRound - 1) / kXRound;
+  q.npr = min(q.nr, kXPieces - q.n_sp);
+  q.n = q.n_sp + q.npr;
+  return q;
+}
+__device__ __forceinline__ bool x_has_piece(uint32_t v) {
+  return (v & kXOpen) && (v & 0xffffu) < ((v >> 16) & 0xffu);
+}
 
 // piece p of P (P = 1: the whole item) runs the chunk's steps [p SA / P, (p + 1) SA / P), SA =
 // steps per chunk; slot >= 0: its partials go to tail slot `slot` of tpart and its IBM bits
@@ -712,14 +761,15 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   const int nstep = min((nframes + FB - 1) / FB, (p + 1) * SA / P);
   // IBM: frames (bit = chunk frame) with decisions deferred to the exact path
   // (ibm_exact_units), OR-ed in LDS by the deciding waves before a step barrier, read after
-  // the item's last one. Two pairs of words used by alternate items: the next item clears its
-  // own before its first barrier, which no thread passes before it has read this item's.
-  uint32_t* const pendw = reinterpret_cast<uint32_t*>(lds + G::MISC_OFF + 32 + 8 * (seq & 1));
+  // the item's last one. Two triples of words used by alternate items: the next item clears
+  // its own before its first barrier, which no thread passes before it has read this item's.
+  uint32_t* const pendw = reinterpret_cast<uint32_t*>(lds + G::MISC_OFF + 32 + 12 * (seq & 1));
   if (MASK == MASK_IBM && tid == 0) {
     int z = 0;
     opaque_i(z);  // formed here (a zero pair held across the items spilled)
     pendw[0] = (uint32_t)z;  // frames with a deferred decision
     pendw[1] = (uint32_t)z;  // frames with uncertain bins in xunc (reference-bit path)
+    pendw[2] = (uint32_t)z;  // of those, frames with kSparseMax or more (round frames)
   }
 
   const typename C::Fft fft = K.fft;
@@ -892,9 +942,13 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
             const int gxi = (Ak.max_frames + kChunk - 1) / kChunk;
             const int unit = slot < 0 ? b * gxi + c : gxi * Ak.batch + slot;
             Ak.xunc[((long long)unit * kChunk + step * FB + my_frame) * 32 + (lane & 31)] = um;
+            int nu = __popc(um);  // the frame's uncertain bins (its lane group's 32 words)
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) nu += __shfl_xor(nu, o, 64);
             if ((lane & 31) == 0) {  // a frame with a deferral, one with its xunc words written
               atomicOr(pendw, 1u << (step * FB + my_frame));
               atomicOr(pendw + 1, 1u << (step * FB + my_frame));
+              if (nu >= kSparseMax) atomicOr(pendw + 2, 1u << (step * FB + my_frame));
             }
           }
         }
@@ -1105,14 +1159,15 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     // deferral, frames with xunc words (reference-bit path), the Nyquist bin's deferrals; the
     // per-bin deferrals
     const uint32_t pend = pendw[0], full = pendw[1];  // block-uniform (after the last barrier)
+    const uint32_t big = REFBITS ? pendw[2] : 0u;       // round frames (published units)
     KArgs& Ak = kernarg_chain_args();  // pointers not held through the loop
     const int gxi = (Ak.max_frames + kChunk - 1) / kChunk;  // analysis_items' units
     const int unit = slot < 0 ? b * gxi + c : gxi * Ak.batch + slot;
     if (nyq_wave && lane == 0) {
-      reinterpret_cast<uint4*>(Ak.xpend)[unit] = make_uint4(pend, full, nyq_dfr, 0u);
+      reinterpret_cast<uint4*>(Ak.xpend)[unit] = make_uint4(pend, full, nyq_dfr, big);
       // the block's units with deferrals, by position in its item sequence (bit 31: any
       // past the 31st); ibm_exact_units reads only their records
-      if (pend) *reinterpret_cast<uint32_t*>(lds + G::MISC_OFF + 48) |= 1u << min(seq, 31);
+      if (pend) *reinterpret_cast<uint32_t*>(lds + G::MISC_OFF + 56) |= 1u << min(seq, 31);
     }
     if (DLT && pend != 0u) {
 #pragma unroll
@@ -1180,6 +1235,36 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
       if constexpr (MASK == MASK_IBM) put_word(N / 2, nyq_bits);
     }
   }
+
+  // ---- a unit with round frames is published for the grid to share (ibm_exact_units): its
+  // record, words, partials and mask words (stored above) released at agent scope first
+  if constexpr (REFBITS) {
+    const uint32_t big = pendw[2];  // block-uniform
+    if (big != 0u) {
+#ifdef AVZ_XTRACE
+      const unsigned long long tp = __builtin_amdgcn_s_memrealtime();
+#endif
+      __syncthreads();
+      if (tid == 0) {
+        KArgs& Ak = kernarg_chain_args();
+        const int gxi = (Ak.max_frames + kChunk - 1) / kChunk;
+        const int unit = slot < 0 ? b * gxi + c : gxi * Ak.batch + slot;
+        const XPieces q = x_pieces(pendw[0], big);
+        Ak.xst[2 * unit + 1] = 0u;  // arrivals
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(Ak.xst + 2 * unit, kXOpen | ((uint32_t)q.n << 16), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or(Ak.xhint + (unit >> 5), 1u << (unit & 31), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+#ifdef AVZ_XTRACE
+        if (g_stamps) {
+          g_stamps[blockIdx.x * 16 + 12] += __builtin_amdgcn_s_memrealtime() - tp;
+          g_stamps[blockIdx.x * 16 + 13] += 1 + 256 * q.n;  // units published, their pieces
+        }
+#endif
+      }
+    }
+  }
 }
 
 // The block's work units: whole items i, i + gridDim.x, ... below a_whole (a multiple of the
@@ -1208,7 +1293,6 @@ __device__ __forceinline__ void analysis_items(const ChainArgs& A, unsigned char
 // per item over the frame's 1024 samples, reduced across the wave. items[]: LDS, f << 16 | k,
 // in frame order; the results go through LDS (res, 6 floats per item) to the bins' threads,
 // which add them to their running sums in item order.
-constexpr int kSparseMax = 12;  // uncertain bins (Nyquist included) a frame decides this way
 template <int N>
 __device__ __forceinline__ void exact_sparse(KArgs& A, unsigned char* lds, int b, int L, int c,
                                              const int* items, int n,
@@ -1350,8 +1434,9 @@ __device__ __forceinline__ void exact_unit(KArgs& A, unsigned char* lds, int u, 
   constexpr int F = N / 2 + 1, NT = G::NT, BPT = G::BPT, FR = XL::FR;
   const int tid = threadIdx.x;
   XSlot* const sl = reinterpret_cast<XSlot*>(lds + XL::SLOT_OFF);
-  const uint32_t pend = reinterpret_cast<const uint4*>(A.xpend)[u].x;  // block-uniform
-  if (pend == 0u) return;
+  const uint4 rec = reinterpret_cast<const uint4*>(A.xpend)[u];  // block-uniform
+  const uint32_t pend = rec.x;
+  if (pend == 0u || (!PER_BIN && rec.w != 0u)) return;  // published: ibm_exact_units' sharing
   int b, c;
   float* const Pt = unit_item<F>(A, u, gx, n_items, n_whole, P, b, c);
   if (A.xstat && tid == 0) atomicAdd(A.xstat, (unsigned long long)__popc(pend));
@@ -1446,6 +1531,255 @@ __device__ __forceinline__ void exact_unit(KArgs& A, unsigned char* lds, int u, 
   }
 }
 
+// The given sparse frames of unit u (reference-bit path), in frame order, in batches of at
+// most XLds::SCAN_INTS (bin, frame) items (exact_sparse) onto the running sums.
+template <int N>
+__device__ __forceinline__ void exact_sparse_frames(KArgs& A, unsigned char* lds, int u, int b,
+                                                    int c, uint32_t frames,
+                                                    Acc32 (&pacc)[CGeo<N>::BPT + 1],
+                                                    uint32_t (&pbits)[CGeo<N>::BPT + 1]) {
+  using G = CGeo<N>;
+  using XL = XLds<N>;
+  const int tid = threadIdx.x;
+  int* const items = reinterpret_cast<int*>(lds + XL::SCAN_OFF);
+  int* const ctl = reinterpret_cast<int*>(lds + XL::CTL_OFF);
+  uint32_t* const wsm = reinterpret_cast<uint32_t*>(lds + 16384);  // [32][32] (slots: free)
+  const uint4 rec = reinterpret_cast<const uint4*>(A.xpend)[u];
+#pragma unroll
+  for (int i = 0; i < kChunk / (G::NT / 32); ++i) {
+    const int f = (tid >> 5) + (G::NT / 32) * i;
+    if ((frames >> f) & 1u)
+      wsm[f * 32 + (tid & 31)] =
+          ((rec.y >> f) & 1u) ? A.xunc[((long long)u * kChunk + f) * 32 + (tid & 31)] : 0u;
+  }
+  __syncthreads();
+  uint32_t todo = frames;
+  while (todo != 0u) {  // block-uniform
+    if (tid < 64) {
+      int base = 0;
+      uint32_t took = 0u;
+      for (uint32_t t = todo; t != 0u; t &= t - 1u) {  // wave-uniform
+        const int f = __builtin_ctz(t);
+        const uint32_t w = tid < 32 ? wsm[f * 32 + tid] : 0u;
+        int inc = __popc(w);
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          const int y = __shfl_up(inc, o, 64);
+          if ((tid & 63) >= o) inc += y;
+        }
+        const int tot = __shfl(inc, 31, 64), ny = (rec.z >> f) & 1u;
+        if (base + tot + ny > XL::SCAN_INTS) break;
+        int at = base + inc - __popc(w);
+        for (uint32_t x = w; x != 0u; x &= x - 1u) items[at++] = (f << 16) | (tid + 32 * __builtin_ctz(x));
+        if (ny && tid == 0) items[base + tot] = (f << 16) | (N / 2);
+        base += tot + ny;
+        took |= 1u << f;
+      }
+      if (tid == 0) {
+        ctl[0] = base;
+        ctl[1] = (int)took;
+      }
+    }
+    __syncthreads();
+    const int n = ctl[0];
+    todo &= ~(uint32_t)ctl[1];
+    exact_sparse<N>(A, lds, b, utt_len(A, b), c, items, n, pacc, pbits);  // ends on a barrier
+  }
+}
+
+// Piece p of published unit u (XPieces): its terms summed from zero, the noise bits OR-ed into
+// the chunk's mask words; with one piece added to the unit's partials at once, otherwise
+// stored (xres[u][p]) and, by the piece that completes the unit (arrivals xst[u].y, agent-scope
+// release / acquire), added to the partials in piece order -- the same sums whichever blocks
+// ran the pieces. The unit's state is reset to 0 when it is complete.
+template <int N>
+__device__ __forceinline__ void exact_piece(KArgs& A, unsigned char* lds, int u, int p, int gx,
+                                            int n_items, int n_whole, int P) {
+  using G = CGeo<N>;
+  using XL = XLds<N>;
+  constexpr int F = N / 2 + 1, NT = G::NT, BPT = G::BPT, FR = XL::FR;
+  const int tid = threadIdx.x;
+  XSlot* const sl = reinterpret_cast<XSlot*>(lds + XL::SLOT_OFF);
+  int* const ctl = reinterpret_cast<int*>(lds + XL::CTL_OFF);
+  const uint4 rec = reinterpret_cast<const uint4*>(A.xpend)[u];  // block-uniform
+  const XPieces q = x_pieces(rec.x, rec.w);
+  int b, c;
+  float* const Pt = unit_item<F>(A, u, gx, n_items, n_whole, P, b, c);
+  Acc32 pacc[BPT + 1];
+  uint32_t pbits[BPT + 1];
+#pragma unroll
+  for (int j = 0; j <= BPT; ++j) {
+    pacc[j].zero();
+    pbits[j] = 0u;
+  }
+  if (p < q.n_sp) {
+    if (A.xstat && tid == 0) atomicAdd(A.xstat, (unsigned long long)__popc(q.sp));  // diagnostic
+    exact_sparse_frames<N>(A, lds, u, b, c, q.sp, pacc, pbits);
+  } else {
+    constexpr int R = kXRound;
+    static_assert(R <= FR, "round frames");
+    const int g = p - q.n_sp, r0 = g * q.nr / q.npr, r1 = (g + 1) * q.nr / q.npr;
+    if (A.xstat && tid == 0)  // diagnostic: the piece's frames
+      atomicAdd(A.xstat, (unsigned long long)(min(R * r1, __popc(rec.w)) - R * r0));
+    const int L = utt_len(A, b);
+    uint32_t rest = rec.w;
+    for (int i = 0; i < r0 * R; ++i) rest &= rest - 1u;
+    for (int r = r0; r < r1; ++r) {  // block-uniform
+      if (tid < R) {  // the round's slots from the record (no per-slot global reads)
+        uint32_t x = rest;
+        for (int i = 0; i < tid && x; ++i) x &= x - 1u;
+        if (x) {
+          const int f = __builtin_ctz(x);
+          XSlot s;
+          s.unit = u;
+          s.f = f;
+          s.e = -1;
+          s.b = b;
+          s.L = L;
+          s.c = c;
+          s.flags = (int)((rec.y >> f) & 1u) | (int)(((rec.z >> f) & 1u) << 1);
+          s.pad = 0;
+          sl[tid] = s;
+        }
+      }
+      const int ns = min(R, __popc(rest));
+      for (int i = 0; i < ns; ++i) rest &= rest - 1u;
+      __syncthreads();
+      exact_round<N, false>(A, lds, sl, ns, pacc, pbits);
+    }
+  }
+  uint32_t* const MW = A.mwords + ((long long)b * A.nchunk + c) * F;
+  float* const R = A.xres + ((long long)u * kXPieces + p) * 5 * F;
+#pragma unroll
+  for (int j = 0; j <= BPT; ++j) {
+    const int kk = j < BPT ? tid + j * NT : N / 2;
+    if (j < BPT || tid == NT - 1) {
+      if (pbits[j]) atomicOr(MW + kk, pbits[j]);
+      if (q.n == 1) {
+        Pt[0 * F + kk] = Pt[0 * F + kk] + pacc[j].c00;
+        Pt[1 * F + kk] = Pt[1 * F + kk] + pacc[j].c11;
+        Pt[2 * F + kk] = Pt[2 * F + kk] + pacc[j].c01r;
+        Pt[3 * F + kk] = Pt[3 * F + kk] + pacc[j].c01i;
+        Pt[4 * F + kk] = Pt[4 * F + kk] + pacc[j].cm;
+      } else {
+        R[0 * F + kk] = pacc[j].c00;
+        R[1 * F + kk] = pacc[j].c11;
+        R[2 * F + kk] = pacc[j].c01r;
+        R[3 * F + kk] = pacc[j].c01i;
+        R[4 * F + kk] = pacc[j].cm;
+      }
+    }
+  }
+#ifdef AVZ_XTRACE
+  const unsigned long long tf = __builtin_amdgcn_s_memrealtime();
+#endif
+  __syncthreads();
+  if (tid == 0) {
+    bool last = true;
+    if (q.n > 1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const uint32_t arrived =
+          __hip_atomic_fetch_add(A.xst + 2 * u + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+      last = arrived == (uint32_t)q.n;
+      if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    ctl[4] = last ? 1 : 0;
+  }
+  __syncthreads();
+#ifdef AVZ_XTRACE
+  const unsigned long long tm = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0 && g_stamps) g_stamps[blockIdx.x * 16 + 6] += tm - tf;
+#endif
+  if (ctl[4]) {  // block-uniform: the unit is complete
+    if (q.n > 1) {
+      // Pt + piece 0 + piece 1 + ... per element; each piece's loads issued together
+      const float* const R0 = A.xres + (long long)u * kXPieces * 5 * F;
+      constexpr int M = (5 * F + NT - 1) / NT;
+      float v[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) v[m] = tid + m * NT < 5 * F ? Pt[tid + m * NT] : 0.0f;
+      for (int pp = 0; pp < q.n; ++pp) {  // block-uniform
+        float t[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+          t[m] = tid + m * NT < 5 * F ? R0[(long long)pp * 5 * F + tid + m * NT] : 0.0f;
+#pragma unroll
+        for (int m = 0; m < M; ++m) v[m] += t[m];
+      }
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (tid + m * NT < 5 * F) Pt[tid + m * NT] = v[m];
+    }
+    if (tid == 0) {
+      __hip_atomic_store(A.xst + 2 * u + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(A.xst + 2 * u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_and(A.xhint + (u >> 5), ~(1u << (u & 31)), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+#ifdef AVZ_XTRACE
+  if (tid == 0 && g_stamps) g_stamps[blockIdx.x * 16 + 7] += __builtin_amdgcn_s_memrealtime() - tm;
+#endif
+}
+
+// One open piece claimed for the block (wave 0; cand: 64 ints of LDS): -1 when no published
+// unit has a piece left. Candidates: the units of the hint bits (from a block-dependent word,
+// at most 64), their states read at once; the block takes one with a piece left (a
+// block-dependent choice among them, so the claimants spread) by adding 1 to its state.
+__device__ __forceinline__ int exact_claim(KArgs& A, int n_units, int* cand) {
+  const int lane = threadIdx.x & 63;
+  const int nw = (n_units + 31) >> 5;
+  const int w_start = (int)(((long long)blockIdx.x * nw) / gridDim.x);
+  for (;;) {  // wave-uniform; a retry follows another block's claim of a unit's last piece
+    int count = 0;
+    for (int w0 = 0; w0 < nw && count < 64; w0 += 64) {  // wave-uniform
+      const int wi = w0 + lane;
+      int wid = w_start + wi;
+      if (wid >= nw) wid -= nw;
+      const uint32_t bits =
+          wi < nw ? __hip_atomic_load(A.xhint + wid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      const int cnt = __popc(bits);
+      int pre = cnt;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(pre, o, 64);
+        if (lane >= o) pre += y;
+      }
+      const int tot = __shfl(pre, 63, 64);
+      int pos = count + pre - cnt;
+      for (uint32_t x = bits; x != 0u && pos < 64; x &= x - 1u) cand[pos++] = wid * 32 + __builtin_ctz(x);
+      count += tot;
+    }
+    count = min(count, 64);
+    if (count == 0) return -1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // cand: LDS, lanes to lanes
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int uid = lane < count ? cand[lane] : -1;
+    const uint32_t v =
+        uid >= 0 ? __hip_atomic_load(A.xst + 2 * uid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const unsigned long long m = __ballot(x_has_piece(v));
+    if (m == 0ull) return -1;
+    int k = (int)(blockIdx.x % (unsigned)__popcll(m));
+    unsigned long long mm = m;
+    for (; k > 0; --k) mm &= mm - 1ull;
+    const int src = __builtin_ctzll(mm);
+    int res = -1;
+    if (lane == src) {
+      const uint32_t old =
+          __hip_atomic_fetch_add(A.xst + 2 * uid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (x_has_piece(old)) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        res = (uid << 8) | (int)(old & 0xffu);
+      }
+    }
+    res = __shfl(res, src, 64);
+    if (res >= 0) return res;
+    __builtin_amdgcn_wave_barrier();  // cand is rewritten by the next scan
+  }
+}
+
 // After the persistent loop: the block's units with deferrals (the unit mask, in
 // analysis_items' order), decided here (exact_unit). Blocks end their loops at different
 // times, so the exact work of one overlaps the others' loops (a separate launch spreading the
@@ -1457,16 +1791,22 @@ __device__ __forceinline__ void ibm_exact_units(unsigned char* lds, int gx, int 
   using XL = XLds<N>;
   constexpr bool SHARE = N == 1024 && !std::is_same<TW, NoTw>::value;
   constexpr bool PER_BIN = !(N == 1024 && !IRM && SHARE);  // not the reference-bit path
+  AVZ_XT(1, __builtin_amdgcn_s_memrealtime());
   if (A.ibm_cert <= 0.0f) return;
   const int tid = threadIdx.x;
   const int P = SPLIT && A.a_pieces > 1 ? A.a_pieces : 1;
   const int n_whole = P > 1 ? A.a_whole : n_items;
   __syncthreads();  // the block's records, partials (global stores of other waves), unit mask
-  const uint32_t mine = *reinterpret_cast<const uint32_t*>(lds + G::MISC_OFF + 48);
-  if (mine == 0u) return;  // block-uniform: no deferral in any of the block's units
-  xtab_fill<N>(A.xtw, A.xwin, reinterpret_cast<cd*>(lds + XL::TWL_OFF),
-               reinterpret_cast<float*>(lds + XL::WIN_OFF), tid, G::NT);
-  __syncthreads();
+  const uint32_t mine = *reinterpret_cast<const uint32_t*>(lds + G::MISC_OFF + 56);
+  if (PER_BIN && mine == 0u) return;  // block-uniform: no deferral in any of the block's units
+  auto tables = [&]() {
+    int t = threadIdx.x;
+    opaque_i(t);  // formed here (a thread index held from the kernel start went to scratch)
+    xtab_fill<N>(A.xtw, A.xwin, reinterpret_cast<cd*>(lds + XL::TWL_OFF),
+                 reinterpret_cast<float*>(lds + XL::WIN_OFF), t, G::NT);
+    __syncthreads();
+  };
+  if (mine != 0u) tables();
   int seq = 0;
   auto one = [&](int u) {
     const int k = seq++;
@@ -1475,6 +1815,52 @@ __device__ __forceinline__ void ibm_exact_units(unsigned char* lds, int gx, int 
   };
   const int n_end = n_whole + (n_items - n_whole) * P;  // analysis_items' sequence
   for (int u = blockIdx.x; u < n_end; u += gridDim.x) one(u < n_whole ? u : n_items + u - n_whole);
+  AVZ_XT(2, __builtin_amdgcn_s_memrealtime());
+  if constexpr (!PER_BIN) {
+    // the published units' pieces, claimed from the whole grid's (the block's own included)
+    // until none is left
+    const int n_units = n_items + (n_end - n_whole);
+    int* const ctl = reinterpret_cast<int*>(lds + XLds<N>::CTL_OFF);
+    bool have_tables = mine != 0u;
+    for (;;) {  // block-uniform
+#ifdef AVZ_XTRACE
+      const unsigned long long tc = __builtin_amdgcn_s_memrealtime();
+#endif
+      if (tid < 64) {
+        const int got = exact_claim(A, n_units, reinterpret_cast<int*>(lds + XLds<N>::SCAN_OFF));
+        if (tid == 0) ctl[2] = got;
+      }
+#ifdef AVZ_XTRACE
+      if (tid == 0 && g_stamps) g_stamps[blockIdx.x * 16 + 14] += __builtin_amdgcn_s_memrealtime() - tc;
+#endif
+      __syncthreads();
+      const int got = ctl[2];
+      __syncthreads();
+      if (got < 0) break;
+      if (!have_tables) {
+#ifdef AVZ_XTRACE
+        const unsigned long long tt = __builtin_amdgcn_s_memrealtime();
+#endif
+        tables();
+        have_tables = true;
+#ifdef AVZ_XTRACE
+        if (tid == 0 && g_stamps) g_stamps[blockIdx.x * 16 + 15] += __builtin_amdgcn_s_memrealtime() - tt;
+#endif
+      }
+#ifdef AVZ_XTRACE
+      const unsigned long long t0x = __builtin_amdgcn_s_memrealtime();
+#endif
+      exact_piece<N>(A, lds, got >> 8, got & 0xff, gx, n_items, n_whole, P);
+#ifdef AVZ_XTRACE
+      if (tid == 0 && g_stamps) {
+        unsigned long long* st = g_stamps + blockIdx.x * 16;
+        st[4] += 1;
+        st[5] += __builtin_amdgcn_s_memrealtime() - t0x;
+      }
+#endif
+    }
+  }
+  AVZ_XT(3, __builtin_amdgcn_s_memrealtime());
 }
 
 // Persistent grid (about two blocks per CU): block i takes the (chunk, utterance) items
@@ -1487,8 +1873,9 @@ template <int N, int MASK, bool IRM, bool SPLIT = false>
 __global__ void __launch_bounds__(kCThreads, KCfg<N>::BLOCKS_PER_CU) avz_analysis_kernel(ChainArgs A) {
   using G = CGeo<N>;
   extern __shared__ __align__(16) unsigned char lds[];
+  AVZ_XT(0, __builtin_amdgcn_s_memrealtime());
   if (MASK == MASK_IBM && threadIdx.x == 0)  // ibm_exact_units' unit mask (after a barrier)
-    *reinterpret_cast<uint32_t*>(lds + G::MISC_OFF + 48) = 0u;
+    *reinterpret_cast<uint32_t*>(lds + G::MISC_OFF + 56) = 0u;
   // the per-utterance synthesis' piece finalize state, reset here (the next launch reads it)
   if (A.pstate)
     for (int b = blockIdx.x * kCThreads + threadIdx.x; b < A.batch; b += gridDim.x * kCThreads)

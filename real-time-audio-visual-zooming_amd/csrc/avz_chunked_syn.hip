@@ -10,7 +10,7 @@ AVZ_SYN_INST(512)
 #undef AVZ_INST
 }  // namespace avz
 
-#ifdef AVZ_STAMPS
+#if defined(AVZ_STAMPS) || defined(AVZ_XTRACE)
 extern "C" int avz_stamps_set_syn(void* p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(avz::g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -3;
 }

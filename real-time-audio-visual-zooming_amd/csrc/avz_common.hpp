@@ -48,6 +48,20 @@ static __device__ unsigned long long* g_stamps;
 #define AVZ_STAMP_INIT() (void)0
 #define AVZ_STAMP(i) (void)0
 #endif
+// Diagnostic build only (-DAVZ_XTRACE: the g_stamps buffer without the phase stamps): thread 0
+// stores absolute s_memrealtime ticks or counts into g_stamps[block][i] (tools/xtrace.py).
+#ifdef AVZ_XTRACE
+#ifndef AVZ_STAMPS
+static __device__ unsigned long long* g_stamps;
+#endif
+#define AVZ_XT(i, v)                                                                    \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && g_stamps)                                                   \
+      g_stamps[(blockIdx.y * gridDim.x + blockIdx.x) * 16 + (i)] = (unsigned long long)(v); \
+  } while (0)
+#else
+#define AVZ_XT(i, v) (void)0
+#endif
 
 // Unchecked-sign form for a wave whose samples are all at index >= 0: the offset is a
 // plain multiple of 4 so the per-register constant folds into the instruction's

@@ -17,6 +17,9 @@ struct PieceState {
 };
 static_assert(sizeof(PieceState) == 16, "one 16-B store resets it");
 
+// Pieces a shared unit of the exact IBM path splits into at most (avz_chunked_k.hpp XPieces).
+constexpr int kXPieces = 8;
+
 struct ChainArgs {
   int batch;
   const int* len;             // [B] samples per utterance (device; kernels clamp to max_len)
@@ -102,6 +105,12 @@ struct ChainArgs {
                               // reference-bit hand-off), written only for units with deferrals
   uint32_t* xunc;             // [units][32 frames][32] reference-bit path: the frame's
                               // uncertain bins (word l bit k: bin l + 32 k), deferred frames only
+  uint32_t* xst;              // [units][2] exact-path work sharing: state, arrivals (zero
+                              // between launches; avz_chunked_k.hpp kXOpen)
+  float* xres;                // [units][kXPieces][5][F] a shared unit's piece sums
+  uint32_t* xhint;            // [units / 32] published units (one bit each)
+  long long xst_reset;        // host-only: bytes of xst to zero before the launch (a caller's
+                              // workspace, whose contents the library does not know)
   int synth_variant;          // host-only (avz_plan_set_diagnostics): synthesis path, 2 default
   void* const* events;        // host-only: (start, stop) hipEvent_t pairs of the 4 launches, or null
   int n_events;               // host-only: how many of them to use (8, or 2: analysis only)

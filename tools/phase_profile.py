@@ -104,3 +104,10 @@ for g in groups:
           f"max {tot.max():.1f}")
     for i, n in enumerate(PHASES):
         print(f"  {n:10s} {us[:, i].mean():8.1f} us  {100*us[:, i].mean()/tot.mean():5.1f} %")
+    if a.exact:  # the exact path runs on few blocks: its critical path is the busiest one's
+        xs = us[:, 4:11].sum(axis=1)
+        busy = np.argsort(-xs)[:6]
+        print(f"exact-path blocks: {int((xs > 0).sum())} of {len(xs)}; busiest (slots 4-10, us):")
+        for r in busy:
+            print(f"  row {r}: total {tot[r]:.1f}, exact {xs[r]:.1f}: "
+                  + " ".join(f"{us[r, i]:.1f}" for i in range(4, 11)))
