@@ -177,3 +177,28 @@ def test_exact_path_ignores_an_earlier_calls_words(avz, gpu_device):
         res.append((out.clone(), peak.clone(), cov))
     for x, y in zip(res[0], res[1]):
         assert torch.equal(torch.nan_to_num(x, nan=7.0), torch.nan_to_num(y, nan=7.0))
+
+
+@pytest.mark.gpu
+def test_work_sharing_state_in_a_callers_workspace(avz, gpu_device):
+    """The exact path's work-sharing state (xst, xhint) must start zero: a caller's workspace
+    arrives with arbitrary bytes, which avz_mvdr_batch clears before the launch. A plan run on
+    a workspace filled with 0xff, twice, gives the plan-workspace result bitwise (utterances
+    4242.. have digital-silence frames: published units, pieces on other blocks)."""
+    from avz import synth
+    S, B = 64000, 64
+    plan = avz.MVDRPlan(n_fft=1024, sigma=1.0, mic_d=0.01, mask="ibm", postfilter="ibm",
+                        normalize="peak", max_batch=B, max_samples=S)
+    dm, dt, di = synth.make_batch_device(B, start=4242, n_samples=S, n_interferers=2,
+                                         device=gpu_device, rng="philox")
+    ws = plan.alloc_workspace(B, S, gpu_device)
+    ws.fill_(0xff)
+    res = []
+    for w in (None, ws, ws):
+        cov = torch.zeros((B, 513, 5), dtype=torch.float64, device=gpu_device)
+        out, peak = plan.run(dm, ref_tgt=dt, ref_int=di, cov_out=cov, workspace=w)
+        torch.cuda.synchronize()
+        res.append((out.clone(), peak.clone(), cov))
+    for r in res[1:]:
+        for x, y in zip(res[0], r):
+            assert torch.equal(torch.nan_to_num(x, nan=7.0), torch.nan_to_num(y, nan=7.0))
