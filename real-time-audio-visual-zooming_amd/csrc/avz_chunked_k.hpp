@@ -1159,7 +1159,9 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
     // deferral, frames with xunc words (reference-bit path), the Nyquist bin's deferrals; the
     // per-bin deferrals
     const uint32_t pend = pendw[0], full = pendw[1];  // block-uniform (after the last barrier)
-    const uint32_t big = REFBITS ? pendw[2] : 0u;       // round frames (published units)
+    // round frames (published units): the reference-bit path's counted ones; every deferred
+    // frame of the per-bin kernels (their exact path is rounds only)
+    const uint32_t big = REFBITS ? pendw[2] : pend;
     KArgs& Ak = kernarg_chain_args();  // pointers not held through the loop
     const int gxi = (Ak.max_frames + kChunk - 1) / kChunk;  // analysis_items' units
     const int unit = slot < 0 ? b * gxi + c : gxi * Ak.batch + slot;
@@ -1237,9 +1239,10 @@ __device__ __forceinline__ void analysis_item(const ChainArgs& A, unsigned char*
   }
 
   // ---- a unit with round frames is published for the grid to share (ibm_exact_units): its
-  // record, words, partials and mask words (stored above) released at agent scope first
-  if constexpr (REFBITS) {
-    const uint32_t big = pendw[2];  // block-uniform
+  // record, words (per-bin deferrals), partials and mask words (stored above) released at
+  // agent scope first
+  if constexpr (MASK == MASK_IBM) {
+    const uint32_t big = REFBITS ? pendw[2] : pendw[0];  // block-uniform
     if (big != 0u) {
 #ifdef AVZ_XTRACE
       const unsigned long long tp = __builtin_amdgcn_s_memrealtime();
@@ -1436,7 +1439,7 @@ __device__ __forceinline__ void exact_unit(KArgs& A, unsigned char* lds, int u, 
   XSlot* const sl = reinterpret_cast<XSlot*>(lds + XL::SLOT_OFF);
   const uint4 rec = reinterpret_cast<const uint4*>(A.xpend)[u];  // block-uniform
   const uint32_t pend = rec.x;
-  if (pend == 0u || (!PER_BIN && rec.w != 0u)) return;  // published: ibm_exact_units' sharing
+  if (pend == 0u || rec.w != 0u) return;  // published: ibm_exact_units' sharing
   int b, c;
   float* const Pt = unit_item<F>(A, u, gx, n_items, n_whole, P, b, c);
   if (A.xstat && tid == 0) atomicAdd(A.xstat, (unsigned long long)__popc(pend));
@@ -1592,7 +1595,7 @@ __device__ __forceinline__ void exact_sparse_frames(KArgs& A, unsigned char* lds
 // stored (xres[u][p]) and, by the piece that completes the unit (arrivals xst[u].y, agent-scope
 // release / acquire), added to the partials in piece order -- the same sums whichever blocks
 // ran the pieces. The unit's state is reset to 0 when it is complete.
-template <int N>
+template <int N, bool PER_BIN>
 __device__ __forceinline__ void exact_piece(KArgs& A, unsigned char* lds, int u, int p, int gx,
                                             int n_items, int n_whole, int P) {
   using G = CGeo<N>;
@@ -1614,7 +1617,7 @@ __device__ __forceinline__ void exact_piece(KArgs& A, unsigned char* lds, int u,
   }
   if (p < q.n_sp) {
     if (A.xstat && tid == 0) atomicAdd(A.xstat, (unsigned long long)__popc(q.sp));  // diagnostic
-    exact_sparse_frames<N>(A, lds, u, b, c, q.sp, pacc, pbits);
+    if constexpr (!PER_BIN) exact_sparse_frames<N>(A, lds, u, b, c, q.sp, pacc, pbits);
   } else {
     constexpr int R = kXRound;
     static_assert(R <= FR, "round frames");
@@ -1637,7 +1640,7 @@ __device__ __forceinline__ void exact_piece(KArgs& A, unsigned char* lds, int u,
           s.b = b;
           s.L = L;
           s.c = c;
-          s.flags = (int)((rec.y >> f) & 1u) | (int)(((rec.z >> f) & 1u) << 1);
+          s.flags = (PER_BIN ? 0 : (int)((rec.y >> f) & 1u)) | (int)(((rec.z >> f) & 1u) << 1);
           s.pad = 0;
           sl[tid] = s;
         }
@@ -1645,7 +1648,7 @@ __device__ __forceinline__ void exact_piece(KArgs& A, unsigned char* lds, int u,
       const int ns = min(R, __popc(rest));
       for (int i = 0; i < ns; ++i) rest &= rest - 1u;
       __syncthreads();
-      exact_round<N, false>(A, lds, sl, ns, pacc, pbits);
+      exact_round<N, PER_BIN>(A, lds, sl, ns, pacc, pbits);
     }
   }
   uint32_t* const MW = A.mwords + ((long long)b * A.nchunk + c) * F;
@@ -1798,7 +1801,6 @@ __device__ __forceinline__ void ibm_exact_units(unsigned char* lds, int gx, int 
   const int n_whole = P > 1 ? A.a_whole : n_items;
   __syncthreads();  // the block's records, partials (global stores of other waves), unit mask
   const uint32_t mine = *reinterpret_cast<const uint32_t*>(lds + G::MISC_OFF + 56);
-  if (PER_BIN && mine == 0u) return;  // block-uniform: no deferral in any of the block's units
   auto tables = [&]() {
     int t = threadIdx.x;
     opaque_i(t);  // formed here (a thread index held from the kernel start went to scratch)
@@ -1806,22 +1808,27 @@ __device__ __forceinline__ void ibm_exact_units(unsigned char* lds, int gx, int 
                  reinterpret_cast<float*>(lds + XL::WIN_OFF), t, G::NT);
     __syncthreads();
   };
-  if (mine != 0u) tables();
+  bool have_tables = false;
   int seq = 0;
-  auto one = [&](int u) {
+  auto one = [&](int u) {  // the block's own unpublished units (published ones are shared)
     const int k = seq++;
     if (!((mine >> min(k, 31)) & 1u)) return;
+    const uint4 rec = reinterpret_cast<const uint4*>(A.xpend)[u];  // block-uniform
+    if (rec.x == 0u || rec.w != 0u) return;
+    if (!have_tables) {
+      tables();
+      have_tables = true;
+    }
     exact_unit<N, PER_BIN>(A, lds, u, gx, n_items, n_whole, P);
   };
   const int n_end = n_whole + (n_items - n_whole) * P;  // analysis_items' sequence
   for (int u = blockIdx.x; u < n_end; u += gridDim.x) one(u < n_whole ? u : n_items + u - n_whole);
   AVZ_XT(2, __builtin_amdgcn_s_memrealtime());
-  if constexpr (!PER_BIN) {
+  {
     // the published units' pieces, claimed from the whole grid's (the block's own included)
     // until none is left
     const int n_units = n_items + (n_end - n_whole);
     int* const ctl = reinterpret_cast<int*>(lds + XLds<N>::CTL_OFF);
-    bool have_tables = mine != 0u;
     for (;;) {  // block-uniform
 #ifdef AVZ_XTRACE
       const unsigned long long tc = __builtin_amdgcn_s_memrealtime();
@@ -1850,7 +1857,7 @@ __device__ __forceinline__ void ibm_exact_units(unsigned char* lds, int gx, int 
 #ifdef AVZ_XTRACE
       const unsigned long long t0x = __builtin_amdgcn_s_memrealtime();
 #endif
-      exact_piece<N>(A, lds, got >> 8, got & 0xff, gx, n_items, n_whole, P);
+      exact_piece<N, PER_BIN>(A, lds, got >> 8, got & 0xff, gx, n_items, n_whole, P);
 #ifdef AVZ_XTRACE
       if (tid == 0 && g_stamps) {
         unsigned long long* st = g_stamps + blockIdx.x * 16;
