@@ -466,6 +466,8 @@ struct XLds {
   static constexpr int WIN_OFF = TWL_OFF + (N / 2) * 16;    // fp32 window [N]
   static constexpr int SLOT_OFF = WIN_OFF + N * 4;           // XSlot[FR], the round's frames
   static constexpr int SCAN_OFF = SLOT_OFF + FR * 32;       // int[256]: exact_sparse's items
+                                                            // (between pieces: exact_claim's
+                                                            // 64 candidates)
   static constexpr int SCAN_INTS = 256;
   static constexpr int WL = 32;                             // frames one block decides
   static constexpr int WL_OFF = SCAN_OFF + 256 * 4;         // int4[WL]: (unit, f, e, -)
@@ -1783,10 +1785,12 @@ __device__ __forceinline__ int exact_claim(KArgs& A, int n_units, int* cand) {
   }
 }
 
-// After the persistent loop: the block's units with deferrals (the unit mask, in
-// analysis_items' order), decided here (exact_unit). Blocks end their loops at different
-// times, so the exact work of one overlaps the others' loops (a separate launch spreading the
-// units over its grid ran 173 us against 159 us this way at kappa 64, configs[1]).
+// After the persistent loop: the block's own unpublished units with deferrals (the unit mask,
+// in analysis_items' order; sparse frames only), decided here (exact_unit), then pieces of the
+// published units claimed from the whole grid (exact_claim, exact_piece) until none is left.
+// Blocks end their loops at different times, so the exact work of one overlaps the others'
+// loops (a separate launch spreading the units over its grid ran 173 us against 159 us at
+// kappa 64, configs[1]; the work sharing took configs[1]'s analysis from 147 to 112 us).
 template <int N, int MASK, bool IRM, bool SPLIT, class TW>
 __device__ __forceinline__ void ibm_exact_units(unsigned char* lds, int gx, int n_items) {
   KArgs& A = kernarg_chain_args();
