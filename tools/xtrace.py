@@ -64,6 +64,12 @@ for rep in range(2):
     print("per piece: finish (barrier, release, arrival) %.1f us, merge %.1f us; publish per unit %.1f us"
           % (x[pc][:, 6].sum() / 100 / npcs, x[pc][:, 7].sum() / 100 / npcs,
              x[pub][:, 12].sum() / 100 / max(1, int((x[pub][:, 13] % 256).sum()))))
+    pubm = x[:, 13] % 256 > 0
+    for name, m in (("publishers", pubm), ("others", ~pubm)):
+        if m.any():
+            print(f"loop end of {name} ({int(m.sum())}): p10 {np.percentile(loop[m], 10):.1f} "
+                  f"p50 {np.percentile(loop[m], 50):.1f} p90 {np.percentile(loop[m], 90):.1f} "
+                  f"max {loop[m].max():.1f} us")
     order = np.argsort(-end)[:8]
     for i in order:
         print(f"  blk {i:4d}: start {us(x[i:i+1, 0])[0]:6.1f} loop {loop[i]:6.1f} own {own[i]:6.1f} "
