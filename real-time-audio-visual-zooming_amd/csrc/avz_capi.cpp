@@ -256,7 +256,7 @@ extern "C" int avz_plan_create(avz_plan** out, const avz_config* cfg) {
     p->xtw = reinterpret_cast<double*>(q + sz_steer);
     p->xwin = reinterpret_cast<float*>(q + sz_steer + sz_xtw);
     ws_layout(c, c.max_batch, p->nchunk, q + sz_tab, &p->ws);
-    if (p->ws.xst) {  // the exact path's work-sharing state starts zero (launches leave it so)
+    if (p->ws.xst) {  // the exact path's work-sharing state starts closed (launches leave it so)
       e = hipMemset(p->ws.xst, 0, p->ws.xst_bytes);
       if (e != hipSuccess) {
         (void)hipFree(p->arena);

@@ -698,8 +698,9 @@ constexpr int kSparseMax = 12;
 // frames (if any), then its rounds of kXRound round frames in up to kXPieces - 1 groups (two
 // frames a round: one fp64 transform per wave, the round's latency about halved against four).
 // xst[u] = {state, arrivals}: state kXOpen | pieces << 16 | next piece while open; claims add
-// 1 (a claim past the last piece, or after the reset, finds no piece: harmless); the piece that
-// completes a unit resets it to 0. xhint: one bit per published unit, cleared with the reset.
+// 1 (a claim past the last piece, or after the reset, finds no piece: harmless; the word stays
+// closed, without kXOpen, and the next publish overwrites it); the piece that completes a unit
+// resets it to 0. xhint: one bit per published unit, cleared with the reset.
 constexpr uint32_t kXOpen = 0x80000000u;
 constexpr int kXRound = 2;
 struct XPieces {

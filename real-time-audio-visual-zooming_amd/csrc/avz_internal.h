@@ -105,7 +105,7 @@ struct ChainArgs {
                               // reference-bit hand-off), written only for units with deferrals
   uint32_t* xunc;             // [units][32 frames][32] reference-bit path: the frame's
                               // uncertain bins (word l bit k: bin l + 32 k), deferred frames only
-  uint32_t* xst;              // [units][2] exact-path work sharing: state, arrivals (zero
+  uint32_t* xst;              // [units][2] exact-path work sharing: state, arrivals (closed
                               // between launches; avz_chunked_k.hpp kXOpen)
   float* xres;                // [units][kXPieces][5][F] a shared unit's piece sums
   uint32_t* xhint;            // [units / 32] published units (one bit each)
